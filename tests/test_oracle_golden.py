@@ -1,0 +1,76 @@
+"""Pin the CPU oracle against the reference's own outputs (tests/golden/)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load():
+    z = np.load(os.path.join(GOLD, "bec_golden.npz"))
+    graphs = {}
+    for gi in range(int(z["num_graphs"][0])):
+        n, k, dv, dc = map(int, z[f"g{gi}_n"])
+        graphs[gi] = (n, k, dv, dc, z[f"g{gi}_v2c"], z[f"g{gi}_c2v"])
+    cases = []
+    for ci in range(int(z["num_cases"][0])):
+        gi, max_its, it, has_err = map(int, z[f"c{ci}_meta"])
+        cases.append(dict(gi=gi, max_its=max_its, it=it, word=z[f"c{ci}_word"], out=z[f"c{ci}_out"],
+                          errors=z[f"c{ci}_errors"], errin=z[f"c{ci}_errin"] if has_err else None))
+    return graphs, cases
+
+
+GRAPHS, CASES = _load()
+
+
+def test_golden_has_cases():
+    assert len(CASES) >= 400 and len(GRAPHS) >= 8
+
+
+@pytest.mark.parametrize("ci", range(0, len(CASES)))
+def test_oracle_message_passing_matches_reference(ci):
+    c = CASES[ci]
+    n, k, dv, dc, v2c, c2v = GRAPHS[c["gi"]]
+    if c["errin"] is None:
+        w, err, it = oracle.message_passing(c["word"], c["max_its"], v2c, c2v, n, k, dv, dc)
+        err = np.insert(err, 0, int(np.count_nonzero(c["word"] == 2)))  # parallel_simulator.py:165
+    else:
+        w, err, it = oracle.message_passing(c["word"], c["max_its"], v2c, c2v, n, k, dv, dc, errors=c["errin"])
+    assert it == c["it"]
+    np.testing.assert_array_equal(w.astype(np.int8), c["out"])
+    np.testing.assert_array_equal(err, c["errors"])
+
+
+def test_oracle_bec_batch_matches_single():
+    n, k, dv, dc, v2c, c2v = GRAPHS[3]
+    sel = [c for c in CASES if c["gi"] == 3 and c["errin"] is None and c["max_its"] == 20]
+    words = np.stack([c["word"] for c in sel])
+    w, err, its = oracle.bec_decode_batch(words, 20, v2c, c2v, n, k, dv, dc)
+    for b, c in enumerate(sel):
+        np.testing.assert_array_equal(w[b], c["out"])
+        np.testing.assert_array_equal(err[b], c["errors"][1:])
+        assert its[b] == c["it"]
+
+
+def test_density_evolution_known_answers():
+    with open(os.path.join(GOLD, "de_golden.json")) as f:
+        g = json.load(f)
+    np.testing.assert_allclose(oracle.density_evolution(0.4, 10, 3, 6), g["density_evolution_0.4_10_3_6"], rtol=1e-12)
+    np.testing.assert_allclose(oracle.density_evolution(0.2, 10, 3, 6, 1e-9), g["density_evolution_0.2_10_3_6_1e-9"], rtol=1e-12)
+    np.testing.assert_allclose(oracle.density_evolution(0.45, 30, 3, 6), g["density_evolution_0.45_30_3_6"], rtol=1e-12)
+    assert abs(g["calc_threshold_3_6"] - 0.42943981) < 1e-7
+
+
+def test_philox_known_answer():
+    # Random123 published known-answer vectors for philox4x32-10 (kat_vectors).
+    np.testing.assert_array_equal(oracle.philox([0, 0, 0, 0], [0, 0]),
+                                  np.array([0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8], np.uint32))
+    np.testing.assert_array_equal(oracle.philox([0xffffffff] * 4, [0xffffffff] * 2),
+                                  np.array([0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd], np.uint32))
+    np.testing.assert_array_equal(
+        oracle.philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0]),
+        np.array([0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1], np.uint32))
