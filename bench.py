@@ -1,0 +1,199 @@
+"""Headline benchmark: decoded codewords/s + info-bit Gb/s, (3,6) n=10000, 50-iteration BP.
+
+Workload (BASELINE.json configs[1]): (3,6)-regular n=10000 (k=5000), BI-AWGN
+channel LLRs (sigma=0.85, Eb/N0 ~ 1.4 dB), fp32 sum-product, batch 65536
+codewords, exactly 50 flooding iterations per codeword (no early stop), one
+MI355X per rank.  One step = one ldpc_bp_decode_batch_dev launch over the
+65536 HBM-resident LLR frames (posterior + hard decision written back).
+Weak scaling: every rank decodes its own 65536-frame batch.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  roofline: SURVEY.md 8(d) algorithmic bytes per
+codeword-iteration B_it = 2*E*4 + 2*n*4 = 320,000 B over the measured average
+kernel duration (HIP events on the launch stream).  cpu_baseline: the oracle's
+OpenMP fp32 sum-product (oracle/ldpc_oracle.c, "port": the reference has no
+soft decoder) on a bounded sample of the same frames.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+N_BITS, DV, DC = 10000, 3, 6
+ITERS = 50
+BATCH = 65536
+SIGMA = 0.85
+HBM_PEAK_GBPS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=BATCH)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(graph, llr_host, seconds):
+    """Oracle fp32 SPA, OpenMP over frames, bounded to ~`seconds` of wall time."""
+    os.environ.setdefault("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1)))
+    from oracle import oracle
+    threads = oracle.num_threads()
+    csr = oracle.csr_from_lists(graph.variable_lookup, graph.check_lookup, graph.n, graph.m, DV, DC)
+    chunk = max(threads, 1) * 2
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        sl = llr_host[done % llr_host.shape[0]:done % llr_host.shape[0] + chunk]
+        if sl.shape[0] < chunk:
+            sl = llr_host[:chunk]
+        oracle.bp_decode_batch(csr, sl, ITERS, 0)
+        done += sl.shape[0]
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": done / el, "unit": "codewords/s", "cores": threads, "kind": "port",
+            "sample": f"{done} frames of the bench workload ((3,6) n=10000 BI-AWGN sigma={SIGMA}, "
+                      f"fp32 sum-product, 50 iterations) in {el:.1f} s, oracle/ldpc_oracle.c OpenMP "
+                      f"x{threads} threads (reference has no soft decoder)"}
+
+
+def load_traffic():
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from iib_project_ldpc_codes_amd import decoder
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+
+    B = args.batch
+    g = TannerGraph.random_regular(N_BITS, DV, DC, seed=1)  # identical code on every rank
+    k = g.k
+    E = g.num_edges
+    stream = torch.cuda.current_stream()
+    llr = decoder.channel_dev("awgn", SIGMA, 2026, rank * B, g.n, B)  # HBM-resident input
+    post = torch.empty_like(llr)
+    hard = torch.empty(llr.shape, dtype=torch.uint8, device=llr.device)
+    its = torch.empty((B,), dtype=torch.int32, device=llr.device)
+
+    def step():
+        decoder.bp_decode_dev(g, llr, ITERS, "spa", early_stop=False, post=post, hard=hard, its=its,
+                              stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    fer = float(hard.any(dim=1).float().mean().item())
+    total_cw = world * B * args.steps
+    value = total_cw / elapsed
+    b_it = 2 * E * 4 + 2 * g.n * 4
+    achieved = b_it * B * ITERS / (kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic()
+
+    extras = {}
+    if not args.no_extras and rank == 0:
+        # same frames with syndrome early termination (max 50 iterations)
+        decoder.bp_decode_dev(g, llr, ITERS, "spa", early_stop=True, post=post, hard=hard, its=its, stream=stream)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        decoder.bp_decode_dev(g, llr, ITERS, "spa", early_stop=True, post=post, hard=hard, its=its, stream=stream)
+        b.record(stream)
+        torch.cuda.synchronize()
+        et_ms = a.elapsed_time(b)
+        extras["early_stop_spa"] = {"codewords_per_s": B / (et_ms * 1e-3),
+                                    "mean_iterations": float(its.float().mean().item())}
+        a.record(stream)
+        decoder.bp_decode_dev(g, llr, ITERS, "minsum", alpha=0.75, post=post, hard=hard, its=its, stream=stream)
+        b.record(stream)
+        torch.cuda.synchronize()
+        extras["minsum_50it_codewords_per_s"] = B / (a.elapsed_time(b) * 1e-3)
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(g, llr[:256].cpu().numpy(), args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "decoded codewords/sec + info-bit Gb/s, (3,6) n=10k 50-iter BP, 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "codewords/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: BI-AWGN LLRs (Philox, all-zero codeword), seeded (3,6) configuration-model code",
+            "config": {"workload": "(3,6)-regular n=10000 BI-AWGN sum-product fp32, batch 65536, 50 iterations "
+                                   "(BASELINE.json configs[1])",
+                       "n": g.n, "k": k, "edges": E, "batch_per_gpu": B, "iterations": ITERS,
+                       "sigma": SIGMA, "early_stop": False, "parallelism": f"trials sharded x{world}",
+                       "kernel": g.kernel_name(False)},
+            "info_bit_gbps": value * k / 1e9,
+            "codeword_iterations_per_s": value * ITERS,
+            "kernel_ms_per_launch": kernel_ms,
+            "fer_at_sigma": fer,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS,
+                         "traffic": traffic.get("bytes_per_launch") if traffic else None,
+                         "algorithmic_bytes_per_codeword_iteration": b_it,
+                         "note": "algorithmic bytes = SURVEY.md 8(d) streaming model; this kernel keeps the "
+                                 "messages in LDS, so HBM traffic is ~80 KB/codeword (see DESIGN.md)"},
+            "cpu_baseline": cpu,
+            "extras": extras,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,515 @@
+// C ABI of libldpc_mi355x.so (declared in include/ldpc_mi355x.h).
+//
+// Host side of the boundary: argument validation, graph preparation (edge
+// lists -> device CSR / slot form), device workspaces and the synchronous
+// host-pointer convenience forms.  There is no CPU compute path: without a
+// visible HIP device every entry point fails with LDPC_ENODEV.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "ldpc_internal.hpp"
+#include "ldpc_mi355x.h"
+
+namespace ldpc {
+namespace {
+thread_local std::string g_err;
+std::mutex g_mu;  // workspaces and the drop-in graph cache
+
+// Grow-only device buffer.
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+        if (e == hipSuccess) cap = bytes;
+        return e;
+    }
+};
+
+struct Workspace {
+    DevBuf trial, its, cutoff, scratch, words, llr, post, hard, errors, itsb;
+};
+std::map<std::pair<int, void *>, Workspace> g_ws;  // (device, stream)
+
+Workspace &workspace(void *stream) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return g_ws[std::make_pair(dev, stream)];
+}
+}  // namespace
+
+void set_error(const std::string &msg) { g_err = msg; }
+}  // namespace ldpc
+
+using namespace ldpc;
+
+#define LDPC_HIP(expr)                                                                            \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess) {                                                                   \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(_e));                         \
+            return LDPC_EHIP;                                                                     \
+        }                                                                                         \
+    } while (0)
+
+#define LDPC_REQUIRE(cond, msg)          \
+    do {                                 \
+        if (!(cond)) {                   \
+            set_error(msg);              \
+            return LDPC_EINVAL;          \
+        }                                \
+    } while (0)
+
+static int require_device() {
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0) {
+        set_error("libldpc_mi355x: no HIP device visible (this library has no CPU path; run on an MI355X)");
+        return LDPC_ENODEV;
+    }
+    return LDPC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Graph preparation
+// ---------------------------------------------------------------------------
+namespace {
+struct HostGraph {
+    int n = 0, m = 0, k = 0, dv = 0, dc = 0;
+    std::vector<int32_t> cvar, cptr, vptr, vchk, vslot;
+    bool consistent = false;
+    int max_vdeg = 0, max_cdeg = 0;
+};
+
+// Regular edge lists in the reference format (random_code_generator.c:34-36, :57-62).
+int host_graph_from_lists(const int32_t *v2c, const int32_t *c2v, int n, int k, int dv, int dc, HostGraph &h) {
+    LDPC_REQUIRE(v2c && c2v, "null edge list");
+    LDPC_REQUIRE(n > 0 && dv > 0 && dc > 0 && k >= 0 && k < n, "bad (n, k, dv, dc)");
+    const int m = n - k;
+    h.n = n; h.m = m; h.k = k; h.dv = dv; h.dc = dc;
+    h.max_vdeg = dv; h.max_cdeg = dc;
+    const size_t Ec = (size_t)m * dc, Ev = (size_t)n * dv;
+    h.cvar.assign(c2v, c2v + Ec);
+    for (size_t e = 0; e < Ec; ++e)
+        LDPC_REQUIRE(h.cvar[e] >= 0 && h.cvar[e] < n, "check_to_variable_list entry out of range [0, n)");
+    for (size_t e = 0; e < Ev; ++e)
+        LDPC_REQUIRE(v2c[e] >= 0 && v2c[e] < m, "variable_to_check_list entry out of range [0, n-k)");
+    h.cptr.resize(m + 1);
+    for (int c = 0; c <= m; ++c) h.cptr[c] = c * dc;
+    h.vptr.resize(n + 1);
+    for (int v = 0; v <= n; ++v) h.vptr[v] = v * dv;
+    h.vchk.resize(Ev);
+    h.vslot.assign(Ev, -1);
+    bool ok = (Ec == Ev);
+    for (int v = 0; v < n; ++v) {
+        for (int j = 0; j < dv; ++j) {
+            const int c = v2c[(size_t)v * dv + j];
+            int occ = 0, rep = 0, found = -1;
+            for (int jj = 0; jj < j; ++jj) rep += (v2c[(size_t)v * dv + jj] == c);
+            for (int s = 0; s < dc; ++s) {
+                if (h.cvar[(size_t)c * dc + s] == v) {
+                    if (occ == rep) found = c * dc + s;
+                    ++occ;
+                }
+            }
+            h.vchk[(size_t)v * dv + j] = occ == 1 ? c : -1;
+            if (found < 0) ok = false;
+            h.vslot[(size_t)v * dv + j] = found;
+        }
+    }
+    h.consistent = ok;
+    return LDPC_OK;
+}
+
+int host_graph_from_csr(const int32_t *cptr, const int32_t *cvar, const int32_t *vptr, const int32_t *vslot, int n,
+                        int m, HostGraph &h) {
+    LDPC_REQUIRE(cptr && cvar && vptr && vslot && n > 0 && m > 0, "bad CSR graph arguments");
+    LDPC_REQUIRE(cptr[0] == 0 && vptr[0] == 0 && cptr[m] == vptr[n] && cptr[m] > 0, "CSR pointers disagree");
+    const int E = cptr[m];
+    h.n = n; h.m = m; h.k = n - m;
+    h.cptr.assign(cptr, cptr + m + 1);
+    h.vptr.assign(vptr, vptr + n + 1);
+    h.cvar.assign(cvar, cvar + E);
+    h.vslot.assign(vslot, vslot + E);
+    std::vector<int32_t> slot_check(E);
+    for (int c = 0; c < m; ++c) {
+        LDPC_REQUIRE(cptr[c + 1] >= cptr[c], "check_ptr not monotone");
+        h.max_cdeg = std::max(h.max_cdeg, cptr[c + 1] - cptr[c]);
+        for (int s = cptr[c]; s < cptr[c + 1]; ++s) {
+            LDPC_REQUIRE(cvar[s] >= 0 && cvar[s] < n, "check_var out of range");
+            slot_check[s] = c;
+        }
+    }
+    std::vector<char> seen(E, 0);
+    h.vchk.resize(E);
+    for (int v = 0; v < n; ++v) {
+        LDPC_REQUIRE(vptr[v + 1] >= vptr[v], "var_ptr not monotone");
+        h.max_vdeg = std::max(h.max_vdeg, vptr[v + 1] - vptr[v]);
+        for (int e = vptr[v]; e < vptr[v + 1]; ++e) {
+            const int s = vslot[e];
+            LDPC_REQUIRE(s >= 0 && s < E && !seen[s] && cvar[s] == v, "var_slot is not a slot permutation");
+            seen[s] = 1;
+            const int c = slot_check[s];
+            int occ = 0;
+            for (int q = cptr[c]; q < cptr[c + 1]; ++q) occ += (cvar[q] == v);
+            h.vchk[e] = occ == 1 ? c : -1;
+        }
+    }
+    bool reg_c = true, reg_v = true;
+    for (int c = 0; c < m; ++c) reg_c &= (cptr[c + 1] - cptr[c] == h.max_cdeg);
+    for (int v = 0; v < n; ++v) reg_v &= (vptr[v + 1] - vptr[v] == h.max_vdeg);
+    if (reg_c && reg_v) {
+        h.dc = h.max_cdeg;
+        h.dv = h.max_vdeg;
+    }
+    h.consistent = true;
+    return LDPC_OK;
+}
+
+template <typename T>
+hipError_t upload(T **dst, const std::vector<T> &src) {
+    *dst = nullptr;
+    if (src.empty()) return hipSuccess;
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(dst), src.size() * sizeof(T));
+    if (e != hipSuccess) return e;
+    return hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+int device_graph(const HostGraph &h, ldpc_graph **out) {
+    int rc = require_device();
+    if (rc) return rc;
+    ldpc_graph *g = new ldpc_graph();
+    g->n = h.n; g->m = h.m; g->k = h.k;
+    g->E = (int)h.cvar.size();
+    g->dv = h.dv; g->dc = h.dc;
+    g->max_vdeg = h.max_vdeg; g->max_cdeg = h.max_cdeg;
+    g->consistent = h.consistent;
+    g->vchk_len = (int)h.vchk.size();
+    (void)hipGetDevice(&g->device);
+    hipError_t e = upload(&g->cvar, h.cvar);
+    if (e == hipSuccess) e = upload(&g->cptr, h.cptr);
+    if (e == hipSuccess) e = upload(&g->vptr, h.vptr);
+    if (e == hipSuccess) e = upload(&g->vchk, h.vchk);
+    if (e == hipSuccess && h.consistent) e = upload(&g->vslot, h.vslot);
+    if (e != hipSuccess) {
+        set_error(std::string("graph upload: ") + hipGetErrorString(e));
+        ldpc_graph_destroy(g);
+        return LDPC_EHIP;
+    }
+    *out = g;
+    return LDPC_OK;
+}
+
+// Drop-in cache: the reference re-sends the same fixed-code lists on every
+// call (parallel_simulator.py:360), so keep the last uploaded graph.
+struct DropInCache {
+    int n = -1, k = -1, dv = -1, dc = -1, dev = -1;
+    uint64_t hash = 0;
+    ldpc_graph *g = nullptr;
+};
+DropInCache g_dropin;
+
+uint64_t fnv(const int32_t *p, size_t len, uint64_t h) {
+    const unsigned char *b = reinterpret_cast<const unsigned char *>(p);
+    for (size_t i = 0; i < len * 4; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+}  // namespace
+
+extern "C" {
+
+const char *ldpc_last_error(void) { return g_err.c_str(); }
+
+int ldpc_device_count(void) {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+    return c;
+}
+
+int ldpc_set_device(int device) {
+    int rc = require_device();
+    if (rc) return rc;
+    LDPC_HIP(hipSetDevice(device));
+    return LDPC_OK;
+}
+
+int ldpc_sync(void *stream) {
+    int rc = require_device();
+    if (rc) return rc;
+    LDPC_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return LDPC_OK;
+}
+
+int ldpc_graph_create(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list, int n, int k,
+                      int dv, int dc, ldpc_graph **out) {
+    LDPC_REQUIRE(out, "null output handle");
+    HostGraph h;
+    int rc = host_graph_from_lists(variable_to_check_list, check_to_variable_list, n, k, dv, dc, h);
+    if (rc) return rc;
+    return device_graph(h, out);
+}
+
+int ldpc_graph_create_csr(const int32_t *check_ptr, const int32_t *check_var, const int32_t *var_ptr,
+                          const int32_t *var_slot, int n, int m, ldpc_graph **out) {
+    LDPC_REQUIRE(out, "null output handle");
+    HostGraph h;
+    int rc = host_graph_from_csr(check_ptr, check_var, var_ptr, var_slot, n, m, h);
+    if (rc) return rc;
+    return device_graph(h, out);
+}
+
+void ldpc_graph_destroy(ldpc_graph *g) {
+    if (!g) return;
+    (void)hipFree(g->cvar);
+    (void)hipFree(g->cptr);
+    (void)hipFree(g->vptr);
+    (void)hipFree(g->vchk);
+    (void)hipFree(g->vslot);
+    delete g;
+}
+
+int ldpc_graph_info(const ldpc_graph *g, int32_t *n, int32_t *m, int32_t *num_edges) {
+    LDPC_REQUIRE(g, "null graph");
+    if (n) *n = g->n;
+    if (m) *m = g->m;
+    if (num_edges) *num_edges = g->E;
+    return LDPC_OK;
+}
+
+const char *ldpc_bp_kernel_name(const ldpc_graph *g, int early_stop) {
+    return g ? bp_kernel_name(*g, early_stop) : "none";
+}
+
+// --------------------------- BEC -------------------------------------------
+int ldpc_bec_decode_batch_dev(const ldpc_graph *g, uint8_t *d_words, int B, int max_iters, int32_t *d_errors,
+                              int32_t *d_its, void *stream) {
+    LDPC_REQUIRE(g && d_words && d_errors && d_its && B >= 0 && max_iters >= 0, "bad BEC batch arguments");
+    if (B == 0 || max_iters == 0) {
+        if (B && d_its) LDPC_HIP(hipMemsetAsync(d_its, 0, sizeof(int32_t) * B, static_cast<hipStream_t>(stream)));
+        return LDPC_OK;
+    }
+    LDPC_HIP(launch_bec_decode(*g, d_words, B, max_iters, d_errors, d_its, static_cast<hipStream_t>(stream)));
+    return LDPC_OK;
+}
+
+static int bec_host(const ldpc_graph *g, uint8_t *words, int B, int max_iters, int32_t *errors, int32_t *its) {
+    const size_t n = g->n;
+    for (size_t i = 0; i < (size_t)B * n; ++i)
+        LDPC_REQUIRE(words[i] <= 2, "channel word value outside {0, 1, 2}");
+    std::lock_guard<std::mutex> lk(g_mu);
+    Workspace &ws = workspace(nullptr);
+    LDPC_HIP(ws.words.ensure((size_t)B * n));
+    LDPC_HIP(ws.errors.ensure(sizeof(int32_t) * (size_t)B * (max_iters > 0 ? max_iters : 1)));
+    LDPC_HIP(ws.itsb.ensure(sizeof(int32_t) * (size_t)B));
+    uint8_t *dw = static_cast<uint8_t *>(ws.words.p);
+    int32_t *de = static_cast<int32_t *>(ws.errors.p), *di = static_cast<int32_t *>(ws.itsb.p);
+    LDPC_HIP(hipMemcpy(dw, words, (size_t)B * n, hipMemcpyHostToDevice));
+    if (max_iters > 0)
+        LDPC_HIP(hipMemcpy(de, errors, sizeof(int32_t) * (size_t)B * max_iters, hipMemcpyHostToDevice));
+    int rc = ldpc_bec_decode_batch_dev(g, dw, B, max_iters, de, di, nullptr);
+    if (rc) return rc;
+    LDPC_HIP(hipDeviceSynchronize());
+    LDPC_HIP(hipMemcpy(words, dw, (size_t)B * n, hipMemcpyDeviceToHost));
+    if (max_iters > 0)
+        LDPC_HIP(hipMemcpy(errors, de, sizeof(int32_t) * (size_t)B * max_iters, hipMemcpyDeviceToHost));
+    LDPC_HIP(hipMemcpy(its, di, sizeof(int32_t) * (size_t)B, hipMemcpyDeviceToHost));
+    return LDPC_OK;
+}
+
+int ldpc_bec_decode_batch(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list, int n,
+                          int k, int dv, int dc, uint8_t *words, int B, int max_iters, int32_t *errors,
+                          int32_t *its) {
+    LDPC_REQUIRE(words && errors && its && B >= 0 && max_iters >= 0, "bad BEC batch arguments");
+    ldpc_graph *g = nullptr;
+    int rc = ldpc_graph_create(variable_to_check_list, check_to_variable_list, n, k, dv, dc, &g);
+    if (rc) return rc;
+    rc = bec_host(g, words, B, max_iters, errors, its);
+    ldpc_graph_destroy(g);
+    return rc;
+}
+
+// Drop-in for message_passing.c:7.
+int message_passing(int *Mvc, int iterations, int *variable_to_check_list, int *check_to_variable_list,
+                    int *errors, int n, int k, int dv, int dc) {
+    if (iterations <= 0) return 0;  // the reference loop body never runs
+    LDPC_REQUIRE(Mvc && errors, "null Mvc / errors");
+    LDPC_REQUIRE(n > 0 && dv > 0 && dc > 0 && k >= 0 && k < n, "bad (n, k, dv, dc)");
+    int rc = require_device();
+    if (rc) return rc;
+    std::vector<uint8_t> w(n);
+    for (int v = 0; v < n; ++v) {
+        LDPC_REQUIRE(Mvc[v] >= 0 && Mvc[v] <= 2, "Mvc value outside {0, 1, 2}");
+        w[v] = (uint8_t)Mvc[v];
+    }
+    ldpc_graph *g = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        const size_t Ev = (size_t)n * dv, Ec = (size_t)(n - k) * dc;
+        uint64_t h = fnv(variable_to_check_list, Ev, 1469598103934665603ull);
+        h = fnv(check_to_variable_list, Ec, h);
+        DropInCache &c = g_dropin;
+        if (!(c.g && c.n == n && c.k == k && c.dv == dv && c.dc == dc && c.dev == dev && c.hash == h)) {
+            if (c.g) ldpc_graph_destroy(c.g);
+            c.g = nullptr;
+            HostGraph hg;
+            rc = host_graph_from_lists(variable_to_check_list, check_to_variable_list, n, k, dv, dc, hg);
+            if (rc) return rc;
+            rc = device_graph(hg, &c.g);
+            if (rc) return rc;
+            c.n = n; c.k = k; c.dv = dv; c.dc = dc; c.dev = dev; c.hash = h;
+        }
+        g = c.g;
+    }
+    int32_t it = 0;
+    rc = bec_host(g, w.data(), 1, iterations, errors, &it);
+    if (rc) return rc;
+    for (int v = 0; v < n; ++v) Mvc[v] = w[v];
+    return it;
+}
+
+// --------------------------- soft ------------------------------------------
+int ldpc_bp_decode_batch_dev(const ldpc_graph *g, const float *d_llr, int B, int max_iters, int algo, float alpha,
+                             int early_stop, float *d_post, uint8_t *d_hard, int32_t *d_its, void *stream) {
+    LDPC_REQUIRE(g && d_llr && B >= 0 && max_iters >= 0, "bad soft batch arguments");
+    LDPC_REQUIRE(algo == LDPC_ALGO_SPA || algo == LDPC_ALGO_MINSUM, "algo must be LDPC_ALGO_SPA or LDPC_ALGO_MINSUM");
+    if (!g->consistent) {
+        set_error("soft decoding needs consistent edge lists (each (v,c) pair listed equally often on both sides)");
+        return LDPC_EINVAL;
+    }
+    if (!strcmp(bp_kernel_name(*g, early_stop), "none")) {
+        set_error("no soft kernel for this graph (check degree > 32)");
+        return LDPC_EUNSUP;
+    }
+    if (B == 0) return LDPC_OK;
+    float *scratch = nullptr;
+    const size_t sb = bp_scratch_bytes(*g, B);
+    if (sb) {
+        std::lock_guard<std::mutex> lk(g_mu);
+        Workspace &ws = workspace(stream);
+        LDPC_HIP(ws.scratch.ensure(sb));
+        scratch = static_cast<float *>(ws.scratch.p);
+    }
+    LDPC_HIP(launch_bp_decode(*g, d_llr, B, max_iters, algo, alpha, early_stop, d_post, d_hard, d_its,
+                              static_cast<hipStream_t>(stream), scratch));
+    return LDPC_OK;
+}
+
+int ldpc_bp_decode_batch(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list, int n, int k,
+                         int dv, int dc, const float *llr, int B, int max_iters, int algo, float alpha,
+                         int early_stop, float *post, uint8_t *hard, int32_t *its) {
+    LDPC_REQUIRE(llr && B >= 0, "bad soft batch arguments");
+    ldpc_graph *g = nullptr;
+    int rc = ldpc_graph_create(variable_to_check_list, check_to_variable_list, n, k, dv, dc, &g);
+    if (rc) return rc;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        Workspace &ws = workspace(nullptr);
+        const size_t nb = (size_t)B * n;
+        hipError_t e = ws.llr.ensure(nb * 4);
+        if (e == hipSuccess) e = ws.post.ensure(nb * 4);
+        if (e == hipSuccess) e = ws.hard.ensure(nb);
+        if (e == hipSuccess) e = ws.itsb.ensure((size_t)B * 4 + 4);
+        if (e == hipSuccess) e = hipMemcpy(ws.llr.p, llr, nb * 4, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            ldpc_graph_destroy(g);
+            set_error(std::string("soft batch staging: ") + hipGetErrorString(e));
+            return LDPC_EHIP;
+        }
+        float *dl = static_cast<float *>(ws.llr.p), *dp = static_cast<float *>(ws.post.p);
+        uint8_t *dh = static_cast<uint8_t *>(ws.hard.p);
+        int32_t *di = static_cast<int32_t *>(ws.itsb.p);
+        rc = 0;
+        // scratch taken inside the _dev call (needs the lock released)
+        if (e == hipSuccess) e = ws.scratch.ensure(bp_scratch_bytes(*g, B));
+        if (B > 0) {
+            e = launch_bp_decode(*g, dl, B, max_iters, algo, alpha, early_stop, dp, dh, di, nullptr,
+                                 static_cast<float *>(ws.scratch.p));
+            if (e == hipSuccess) e = hipDeviceSynchronize();
+            if (e == hipSuccess && post) e = hipMemcpy(post, dp, nb * 4, hipMemcpyDeviceToHost);
+            if (e == hipSuccess && hard) e = hipMemcpy(hard, dh, nb, hipMemcpyDeviceToHost);
+            if (e == hipSuccess && its) e = hipMemcpy(its, di, (size_t)B * 4, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) {
+                set_error(std::string("soft batch: ") + hipGetErrorString(e));
+                rc = LDPC_EHIP;
+            }
+        }
+    }
+    ldpc_graph_destroy(g);
+    return rc;
+}
+
+// --------------------------- channels / MC ---------------------------------
+static int channel_params(int channel, float param, float *p, float *p2) {
+    LDPC_REQUIRE(channel >= 0 && channel <= 2, "channel must be LDPC_CH_BEC, LDPC_CH_BSC or LDPC_CH_AWGN");
+    *p = param;
+    *p2 = 0.0f;
+    if (channel == LDPC_CH_BSC) {
+        LDPC_REQUIRE(param > 0.0f && param < 0.5f, "BSC crossover probability must be in (0, 0.5)");
+        *p2 = (float)std::log((1.0 - (double)param) / (double)param);
+    } else if (channel == LDPC_CH_AWGN) {
+        LDPC_REQUIRE(param > 0.0f, "AWGN sigma must be > 0");
+        *p2 = (float)(2.0 / ((double)param * (double)param));
+    } else {
+        LDPC_REQUIRE(param >= 0.0f && param <= 1.0f, "erasure probability must be in [0, 1]");
+    }
+    return LDPC_OK;
+}
+
+int ldpc_channel_dev(int channel, float param, uint64_t seed, uint64_t first_cw, int n, int B, void *d_out,
+                     void *stream) {
+    LDPC_REQUIRE(d_out && n > 0 && B >= 0, "bad channel arguments");
+    float p, p2;
+    int rc = channel_params(channel, param, &p, &p2);
+    if (rc) return rc;
+    LDPC_HIP(launch_channel(channel, p, p2, seed, first_cw, n, B, d_out, static_cast<hipStream_t>(stream)));
+    return LDPC_OK;
+}
+
+int ldpc_mc_batch_dev(const ldpc_graph *g, int channel, float param, uint64_t seed, uint64_t first_cw, int B,
+                      int max_iters, int algo, float alpha, int early_stop, int expurgation,
+                      int64_t stop_frame_errors, int64_t *d_counters, void *stream) {
+    LDPC_REQUIRE(g && d_counters && B >= 0 && max_iters >= 0, "bad MC arguments");
+    float p, p2;
+    int rc = channel_params(channel, param, &p, &p2);
+    if (rc) return rc;
+    if (channel != LDPC_CH_BEC) {
+        LDPC_REQUIRE(algo == LDPC_ALGO_SPA || algo == LDPC_ALGO_MINSUM, "bad algo");
+        LDPC_REQUIRE(g->consistent, "soft decoding needs consistent edge lists");
+    }
+    if (B == 0) return LDPC_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(g_mu);
+    Workspace &ws = workspace(stream);
+    LDPC_HIP(ws.trial.ensure(sizeof(int32_t) * (size_t)B * (max_iters + 1)));
+    LDPC_HIP(ws.its.ensure(sizeof(int32_t) * (size_t)B));
+    LDPC_HIP(ws.cutoff.ensure(16));
+    float *scratch = nullptr;
+    if (channel != LDPC_CH_BEC) {
+        const size_t sb = bp_scratch_bytes(*g, B);
+        if (sb) {
+            LDPC_HIP(ws.scratch.ensure(sb));
+            scratch = static_cast<float *>(ws.scratch.p);
+        }
+    }
+    int32_t *trial = static_cast<int32_t *>(ws.trial.p), *its = static_cast<int32_t *>(ws.its.p);
+    LDPC_HIP(launch_mc_decode(*g, channel, p, p2, seed, first_cw, B, max_iters, algo, alpha, early_stop, trial, its,
+                              s, scratch));
+    LDPC_HIP(launch_mc_reduce(trial, its, B, max_iters, expurgation, stop_frame_errors, d_counters,
+                              static_cast<int32_t *>(ws.cutoff.p), s));
+    return LDPC_OK;
+}
+
+}  // extern "C"

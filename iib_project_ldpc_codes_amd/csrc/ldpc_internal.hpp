@@ -1,0 +1,60 @@
+// Internal declarations shared by the C ABI (capi.cpp) and the kernels
+// (ldpc_kernels.hip).  Not part of the public ABI (see include/ldpc_mi355x.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+// Device-resident Tanner graph.  Slot e = position in the check-major edge
+// list (the reference's check_lookup order, random_code_generator.c:34-36).
+struct ldpc_graph {
+    int n = 0, m = 0, k = 0, E = 0;
+    int dv = 0, dc = 0;          // > 0 when every variable / check has that degree
+    int max_vdeg = 0, max_cdeg = 0;
+    bool consistent = false;     // vslot defined: soft decoding allowed
+    int device = 0;
+    // device arrays
+    int32_t *cvar = nullptr;     // [E]   variable of each slot (check-major)
+    int32_t *cptr = nullptr;     // [m+1] check c owns slots [cptr[c], cptr[c+1])
+    int32_t *vptr = nullptr;     // [n+1] variable v owns edges [vptr[v], vptr[v+1])
+    int32_t *vchk = nullptr;     // [E']  BEC: check id of each variable edge, -1 when
+                                 //       that check holds v != 1 times (never assigns)
+    int32_t *vslot = nullptr;    // [E]   soft: slot of each variable edge (consistent only)
+    int vchk_len = 0;
+};
+
+namespace ldpc {
+
+void set_error(const std::string &msg);
+
+// Kernel launchers (ldpc_kernels.hip).  All asynchronous on `stream`.
+// Return hipSuccess or the launch error.
+hipError_t launch_bec_decode(const ldpc_graph &g, uint8_t *d_words, int B, int max_iters,
+                             int32_t *d_errors, int32_t *d_its, hipStream_t stream);
+
+hipError_t launch_bp_decode(const ldpc_graph &g, const float *d_llr, int B, int max_iters, int algo,
+                            float alpha, int early_stop, float *d_post, uint8_t *d_hard,
+                            int32_t *d_its, hipStream_t stream, float *d_scratch);
+
+// Bytes of global scratch launch_bp_decode needs for this graph/batch (0 when
+// the messages fit in LDS).
+size_t bp_scratch_bytes(const ldpc_graph &g, int B);
+
+hipError_t launch_channel(int channel, float p, float p2, uint64_t seed, uint64_t first_cw, int n,
+                          int B, void *d_out, hipStream_t stream);
+
+// Monte-Carlo: fused channel + decode writing per-trial curves into `trial`
+// ([B][max_iters+1] int32) and its into `trial_its` ([B]); then the reducer.
+hipError_t launch_mc_decode(const ldpc_graph &g, int channel, float p, float p2, uint64_t seed,
+                            uint64_t first_cw, int B, int max_iters, int algo, float alpha,
+                            int early_stop, int32_t *trial, int32_t *trial_its, hipStream_t stream,
+                            float *d_scratch);
+hipError_t launch_mc_reduce(const int32_t *trial, const int32_t *trial_its, int B, int max_iters,
+                            int expurgation, int64_t stop_frame_errors, int64_t *d_counters,
+                            int32_t *d_cutoff, hipStream_t stream);
+
+// Kernel-choice introspection for tests / bench ("lds36", "generic", ...).
+const char *bp_kernel_name(const ldpc_graph &g, int early_stop);
+
+}  // namespace ldpc

@@ -1,0 +1,935 @@
+// HIP kernels for gfx950 (MI355X): BEC erasure decoding, soft flooding BP
+// (sum-product / normalized min-sum), on-device channels and Monte-Carlo
+// statistics.  Layout and rationale: DESIGN.md.
+//
+// Reference behaviour restated here:
+//   message_passing.c:7-82         -> bec_kernel           (bit-exact)
+//   channels.py:24-26 new_transmit -> channel_kernel / chan_* (same law, Philox)
+//   parallel_simulator.py:198-244  -> mc_* (per-trial statistics + stop rule)
+#include <rocrand/rocrand_kernel.h>
+
+#include "ldpc_internal.hpp"
+#include "ldpc_mi355x.h"
+
+namespace ldpc {
+namespace {
+
+constexpr float kPMax = 0.99999994f;  // 1 - 2^-24, as oracle/ldpc_oracle.c
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (the rocRAND philox4x32_10 stream: rocrand_init(seed,
+// subsequence = codeword, offset = 4*g) -> rocrand4 == philox_block(g, 0,
+// cw_lo, cw_hi) under key {seed_lo, seed_hi}).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ float u01(uint32_t x) {
+    return (float)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8f;
+}
+
+struct ChanArgs {
+    int kind;      // LDPC_CH_*
+    float p, p2;   // see oracle_channel
+    uint32_t k0, k1;
+};
+
+__device__ __forceinline__ uint32_t pick4(uint4 r, int i) {
+    return i == 0 ? r.x : (i == 1 ? r.y : (i == 2 ? r.z : r.w));
+}
+
+// Channel value of variable v of codeword cw (all-zero codeword sent).
+__device__ __forceinline__ float chan_soft(const ChanArgs &ch, uint64_t cw, int v) {
+    const uint4 r = philox_block((uint32_t)(v >> 2), 0u, (uint32_t)cw, (uint32_t)(cw >> 32), ch.k0, ch.k1);
+    const int i = v & 3;
+    if (ch.kind == 1) return u01(pick4(r, i)) < ch.p ? -ch.p2 : ch.p2;
+    const int h = i >> 1;
+    const float ua = u01(h ? r.z : r.x), ub = u01(h ? r.w : r.y);
+    const float rad = sqrtf(-2.0f * logf(ua));
+    const float ang = 6.28318530717958647692f * ub;
+    const float g = rad * ((i & 1) ? sinf(ang) : cosf(ang));
+    return (1.0f + ch.p * g) * ch.p2;
+}
+
+__device__ __forceinline__ uint8_t chan_bec(const ChanArgs &ch, uint64_t cw, int v) {
+    const uint4 r = philox_block((uint32_t)(v >> 2), 0u, (uint32_t)cw, (uint32_t)(cw >> 32), ch.k0, ch.k1);
+    return u01(pick4(r, v & 3)) < ch.p ? 2 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Block reductions (wave64)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wave_sum(int x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
+    return x;
+}
+
+template <int T>
+__device__ __forceinline__ int block_sum(int x, int *red) {
+    x = wave_sum(x);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = x;
+    __syncthreads();
+    int s = 0;
+#pragma unroll
+    for (int w = 0; w < T / kWave; ++w) s += red[w];
+    __syncthreads();
+    return s;
+}
+
+// ===========================================================================
+// 1. BEC erasure decoding -- message_passing.c:7-82, bit-exact.
+//
+// One workgroup per codeword.  LDS: caller errors[] (int32), the ternary word
+// (u8) and one byte per check.  The reference's per-slot check messages are
+// never materialised: a slot addressed to an ERASED variable is known iff its
+// check holds exactly one erasure, and then equals the parity of the check's
+// known bits (message_passing.c:31-43); so each check publishes one byte
+// cs = ne==1 ? parity : 2 and an erased variable takes the last cs != 2 over
+// its checks in variable_to_check_list order (message_passing.c:55-62).
+// vchk = -1 marks a (variable, check) pair where the check does not hold the
+// variable exactly once: such a pair never assigns in the reference.
+// ===========================================================================
+struct BecArgs {
+    const int32_t *cvar, *cptr, *vptr, *vchk;
+    int n, m, dv, dc;  // dv, dc > 0: regular (pointers implicit)
+    uint8_t *words;
+    int32_t *errors, *its;
+    int max_iters;
+    // Monte-Carlo mode
+    ChanArgs ch;
+    uint64_t first_cw;
+    int32_t *trial;  // [B][max_iters+1]
+};
+
+template <int T, bool MC>
+__global__ __launch_bounds__(T) void bec_kernel(BecArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int red[T / kWave];
+    const int tid = threadIdx.x;
+    const size_t b = blockIdx.x;
+    const int n = a.n, m = a.m, iters = a.max_iters;
+    int32_t *errs = reinterpret_cast<int32_t *>(smem);
+    uint8_t *mvc = smem + ((iters * 4 + 15) & ~15);
+    uint8_t *cs = mvc + ((n + 15) & ~15);
+
+    int init_cnt = 0;
+    if (MC) {
+        const uint64_t cw = a.first_cw + b;
+        for (int v = tid; v < n; v += T) {
+            const uint8_t x = chan_bec(a.ch, cw, v);
+            mvc[v] = x;
+            init_cnt += (x == 2);
+        }
+        for (int i = tid; i < iters; i += T) errs[i] = 0;
+    } else {
+        const uint8_t *w = a.words + b * n;
+        for (int v = tid; v < n; v += T) mvc[v] = w[v];
+        const int32_t *e = a.errors + b * iters;
+        for (int i = tid; i < iters; i += T) errs[i] = e[i];
+    }
+    __syncthreads();
+    const int initial = MC ? block_sum<T>(init_cnt, red) : 0;
+
+    int prev1 = 0, prev2 = 0;  // errors[it-1], errors[it-2] after accumulation
+    int it;
+    for (it = 0; it < iters; ++it) {
+        if (it >= 2 && prev1 == prev2) {  // message_passing.c:16-19 (absorbing)
+            for (int i = it + tid; i < iters; i += T) errs[i] = prev1;
+            it = iters;
+            break;
+        }
+        // check phase (reads the previous word only)
+        for (int c = tid; c < m; c += T) {
+            const int s0 = a.dc > 0 ? c * a.dc : a.cptr[c];
+            const int s1 = a.dc > 0 ? s0 + a.dc : a.cptr[c + 1];
+            int ne = 0, par = 0;
+            for (int s = s0; s < s1; ++s) {
+                const int x = mvc[a.cvar[s]];
+                ne += (x == 2);
+                par ^= (x & 1);
+            }
+            cs[c] = (uint8_t)(ne == 1 ? par : 2);
+        }
+        __syncthreads();
+        // variable phase: erased variables take the last known check message
+        int cnt = 0;
+        for (int v = tid; v < n; v += T) {
+            int x = mvc[v];
+            if (x == 2) {
+                const int e0 = a.dv > 0 ? v * a.dv : a.vptr[v];
+                const int e1 = a.dv > 0 ? e0 + a.dv : a.vptr[v + 1];
+                for (int e = e0; e < e1; ++e) {
+                    const int c = a.vchk[e];
+                    if (c >= 0) {
+                        const int y = cs[c];
+                        if (y != 2) x = y;
+                    }
+                }
+                mvc[v] = (uint8_t)x;
+                cnt += (x == 2);
+            }
+        }
+        const int base = errs[it];  // read before block_sum's barriers, written after
+        const int total = block_sum<T>(cnt, red);
+        const int cur = base + total;
+        if (tid == 0) errs[it] = cur;
+        prev2 = prev1;
+        prev1 = cur;
+        if (total == 0) break;  // message_passing.c:76-78
+    }
+    __syncthreads();
+    if (MC) {
+        int32_t *tr = a.trial + b * (size_t)(iters + 1);
+        for (int i = tid; i <= iters; i += T) tr[i] = i == 0 ? initial : errs[i - 1];
+        if (tid == 0) a.its[b] = it;
+    } else {
+        uint8_t *w = a.words + b * n;
+        for (int v = tid; v < n; v += T) w[v] = mvc[v];
+        int32_t *e = a.errors + b * iters;
+        for (int i = tid; i < iters; i += T) e[i] = errs[i];
+        if (tid == 0) a.its[b] = it;
+    }
+}
+
+// ===========================================================================
+// 2. Soft flooding BP (no reference counterpart; oracle_bp_decode defines it)
+// ===========================================================================
+__device__ __forceinline__ float tanh_half(float x) {
+    const float e = __expf(-fabsf(x));
+    const float t = __fdividef(1.0f - e, 1.0f + e);
+    return x < 0.0f ? -t : t;
+}
+
+__device__ __forceinline__ float atanh2(float p) {
+    p = fminf(fmaxf(p, -kPMax), kPMax);
+    return __logf(__fdividef(1.0f + p, 1.0f - p));
+}
+
+// Check-node update over D messages in registers (padding: +inf, neutral for
+// both rules).  Same operation order as oracle check_update_{spa,ms}.
+template <int ALGO, int D>
+__device__ __forceinline__ void check_update(float (&x)[D], float alpha) {
+    if (ALGO == 0) {
+        float t[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) t[i] = tanh_half(x[i]);
+        float pre[D], suf[D];
+        pre[0] = 1.0f;
+#pragma unroll
+        for (int i = 1; i < D; ++i) pre[i] = pre[i - 1] * t[i - 1];
+        suf[D - 1] = 1.0f;
+#pragma unroll
+        for (int i = D - 2; i >= 0; --i) suf[i] = suf[i + 1] * t[i + 1];
+#pragma unroll
+        for (int i = 0; i < D; ++i) x[i] = atanh2(pre[i] * suf[i]);
+    } else {
+        float m1 = __builtin_inff(), m2 = __builtin_inff();
+        int i1 = 0, neg = 0;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            const float a = fabsf(x[i]);
+            neg ^= (x[i] < 0.0f);
+            if (a < m1) { m2 = m1; m1 = a; i1 = i; }
+            else if (a < m2) { m2 = a; }
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            const float mag = alpha * (i == i1 ? m2 : m1);
+            x[i] = (neg ^ (x[i] < 0.0f)) ? -mag : mag;
+        }
+    }
+}
+
+struct BpArgs {
+    const int32_t *cptr, *cvar, *vptr, *vslot;
+    int n, m, E, B;
+    const float *llr;
+    float *post;
+    uint8_t *hard;
+    int32_t *its;
+    int max_iters;
+    float alpha;
+    // Monte-Carlo mode
+    ChanArgs ch;
+    uint64_t first_cw;
+    int32_t *trial;  // [B][max_iters+1]
+    // generic kernel, messages in global scratch
+    float *scratch;
+};
+
+// ---------------------------------------------------------------------------
+// 2a. Regular fast path: whole codeword resident in LDS.
+//   LDS  msg[E] fp32 (check-major slots: check c = [c*DC, c*DC+DC)),
+//        hs[E] u8 hard decision per slot (ET / MC only), curve (MC only).
+//   Thread t owns checks t, t+T, ... and variables t + i*T (i < VPT); its
+//   variables' slot indices and channel LLRs stay in VGPRs for the whole
+//   decode.  Iteration = check phase (contiguous float2 LDS traffic, tanh /
+//   min-sum in registers) | barrier | variable phase (DV random LDS gathers,
+//   posterior, extrinsic write-back) | barrier.
+// ---------------------------------------------------------------------------
+template <int DV, int DC, int T, int VPT, int ALGO, bool ET, bool MC>
+__global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    float *msg = reinterpret_cast<float *>(smem);
+    uint8_t *hs = smem + (size_t)a.E * 4;
+    int *curve = reinterpret_cast<int *>(smem + (((size_t)a.E * 5 + 15) & ~(size_t)15));
+    const int tid = threadIdx.x;
+    const int n = a.n, m = a.m, iters = a.max_iters;
+    constexpr int NS = VPT * DV;            // slots owned through my variables
+    constexpr bool KEEP_POST = ET && !MC;   // posterior must survive the loop
+
+    for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+        const uint64_t cw = a.first_cw + (uint64_t)b;
+        // slot indices packed two per VGPR (E < 65536 on this path)
+        uint32_t sp[(NS + 1) / 2];
+        float L[VPT];
+        float pr[KEEP_POST ? VPT : 1];
+        int err0 = 0;
+#pragma unroll
+        for (int q = 0; q < (NS + 1) / 2; ++q) sp[q] = 0;
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            const int v = tid + i * T;
+            L[i] = 0.0f;
+            if (v < n) {
+                L[i] = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
+                err0 += (L[i] < 0.0f);
+#pragma unroll
+                for (int j = 0; j < DV; ++j) {
+                    const int q = i * DV + j;
+                    sp[q >> 1] |= (uint32_t)a.vslot[v * DV + j] << (16 * (q & 1));
+                }
+            }
+            if constexpr (KEEP_POST) pr[i] = L[i];
+        }
+#define SLOT(i, j) ((int)((sp[((i) * DV + (j)) >> 1] >> (16 * (((i) * DV + (j)) & 1))) & 0xFFFFu))
+        __syncthreads();  // previous codeword fully drained (msg, curve)
+        if (MC) {
+            for (int i = tid; i <= iters; i += T) curve[i] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            if (tid + i * T < n) {
+#pragma unroll
+                for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = L[i];
+            }
+        }
+        __syncthreads();
+        if (MC) {
+            const int w = wave_sum(err0);
+            if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[0], w);
+        }
+        if (!ET && !MC && iters == 0) {
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) {
+                const int v = tid + i * T;
+                if (v < n) {
+                    if (a.post) a.post[(size_t)b * n + v] = L[i];
+                    if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(L[i] < 0.0f);
+                }
+            }
+        }
+
+        int it = 0;
+        for (; it < iters; ++it) {
+            if (ET && it > 0) {  // syndrome of the previous iteration's hard decision
+                int unsat = 0;
+                for (int c = tid; c < m; c += T) {
+                    int par = 0;
+#pragma unroll
+                    for (int s = 0; s < DC; ++s) par ^= hs[c * DC + s];
+                    unsat |= par;
+                }
+                if (!__syncthreads_or(unsat)) break;
+            } else if (it > 0) {
+                __syncthreads();
+            }
+            // check phase
+            for (int c = tid; c < m; c += T) {
+                float x[DC];
+                if constexpr (DC % 2 == 0) {
+                    const float2 *p = reinterpret_cast<const float2 *>(msg + c * DC);
+#pragma unroll
+                    for (int q = 0; q < DC / 2; ++q) {
+                        const float2 y = p[q];
+                        x[2 * q] = y.x;
+                        x[2 * q + 1] = y.y;
+                    }
+                } else {
+#pragma unroll
+                    for (int s = 0; s < DC; ++s) x[s] = msg[c * DC + s];
+                }
+                check_update<ALGO, DC>(x, a.alpha);
+                if constexpr (DC % 2 == 0) {
+                    float2 *p = reinterpret_cast<float2 *>(msg + c * DC);
+#pragma unroll
+                    for (int q = 0; q < DC / 2; ++q) p[q] = make_float2(x[2 * q], x[2 * q + 1]);
+                } else {
+#pragma unroll
+                    for (int s = 0; s < DC; ++s) msg[c * DC + s] = x[s];
+                }
+            }
+            __syncthreads();
+            // variable phase.  Launder the packed slots so the compiler cannot
+            // hoist their unpacking out of the iteration loop (that would pin
+            // VPT*DV unpacked addresses in VGPRs and spill).
+#pragma unroll
+            for (int q = 0; q < (NS + 1) / 2; ++q) asm volatile("" : "+v"(sp[q]));
+            const bool final_it = !ET && !MC && it == iters - 1;
+            int errs = 0;
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) {
+                const int v = tid + i * T;
+                if (v < n) {
+                    float cv[DV];
+                    float s = L[i];
+#pragma unroll
+                    for (int j = 0; j < DV; ++j) {
+                        cv[j] = msg[SLOT(i, j)];
+                        s += cv[j];
+                    }
+                    if (final_it) {
+                        if (a.post) a.post[(size_t)b * n + v] = s;
+                        if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = s - cv[j];
+                    }
+                    if constexpr (KEEP_POST) pr[i] = s;
+                    if (ET) {
+#pragma unroll
+                        for (int j = 0; j < DV; ++j) hs[SLOT(i, j)] = (uint8_t)(s < 0.0f);
+                    }
+                    errs += (s < 0.0f);
+                }
+                // keep at most two variables' gathers in flight per thread:
+                // bounds VGPRs at 4 waves/SIMD (16 waves/CU hide the LDS latency)
+                if (i & 1) __builtin_amdgcn_sched_barrier(0);
+            }
+            if (MC) {
+                const int w = wave_sum(errs);
+                if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[it + 1], w);
+            }
+        }
+#undef SLOT
+        if (MC) {
+            __syncthreads();
+            int32_t *tr = a.trial + (size_t)b * (iters + 1);
+            const int last = curve[it];
+            for (int i = tid; i <= iters; i += T) tr[i] = i <= it ? curve[i] : last;
+            if (tid == 0) a.its[b] = it;
+        } else {
+            if constexpr (KEEP_POST) {
+#pragma unroll
+                for (int i = 0; i < VPT; ++i) {
+                    const int v = tid + i * T;
+                    if (v < n) {
+                        if (a.post) a.post[(size_t)b * n + v] = pr[i];
+                        if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(pr[i] < 0.0f);
+                    }
+                }
+            }
+            if (a.its && tid == 0) a.its[b] = it;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 2b. Generic path: any (irregular) CSR graph, check degree <= MAXDC.
+//   Messages in LDS when they fit, else in a per-workgroup global scratch
+//   slab (GMEM; the slab stays L2 / Infinity-Cache resident).  Channel LLRs
+//   are kept beside the messages.  Posterior / hard decision are written to
+//   the outputs after every variable phase.
+// ---------------------------------------------------------------------------
+template <int T, int MAXDC, int ALGO, bool ET, bool MC, bool GMEM>
+__global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int n = a.n, m = a.m, E = a.E, iters = a.max_iters;
+    unsigned char *base = GMEM ? reinterpret_cast<unsigned char *>(a.scratch) +
+                                     (size_t)blockIdx.x * (((size_t)E * 5 + (size_t)n * 4 + 15) & ~(size_t)15)
+                               : smem;
+    float *msg = reinterpret_cast<float *>(base);
+    float *Ls = msg + E;
+    uint8_t *hs = reinterpret_cast<uint8_t *>(Ls + n);
+    int *curve = reinterpret_cast<int *>(GMEM ? smem : smem + (((size_t)E * 5 + (size_t)n * 4 + 15) & ~(size_t)15));
+
+    for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+        const uint64_t cw = a.first_cw + (uint64_t)b;
+        __syncthreads();  // previous codeword fully drained
+        if (MC) {
+            for (int i = tid; i <= iters; i += T) curve[i] = 0;
+        }
+        __syncthreads();
+        int err0 = 0;
+        for (int v = tid; v < n; v += T) {
+            const float l = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
+            Ls[v] = l;
+            err0 += (l < 0.0f);
+            for (int e = a.vptr[v]; e < a.vptr[v + 1]; ++e) msg[a.vslot[e]] = l;
+            if (!MC) {
+                if (a.post) a.post[(size_t)b * n + v] = l;
+                if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(l < 0.0f);
+            }
+        }
+        if (MC) {
+            const int w = wave_sum(err0);
+            if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[0], w);
+        }
+        __syncthreads();
+        int it = 0;
+        for (; it < iters; ++it) {
+            if (ET && it > 0) {
+                int unsat = 0;
+                for (int c = tid; c < m; c += T) {
+                    int par = 0;
+                    for (int s = a.cptr[c]; s < a.cptr[c + 1]; ++s) par ^= hs[s];
+                    unsat |= par;
+                }
+                if (!__syncthreads_or(unsat)) break;
+            } else if (it > 0) {
+                __syncthreads();
+            }
+            for (int c = tid; c < m; c += T) {
+                const int s0 = a.cptr[c], d = a.cptr[c + 1] - s0;
+                float x[MAXDC];
+#pragma unroll
+                for (int s = 0; s < MAXDC; ++s) x[s] = s < d ? msg[s0 + s] : __builtin_inff();
+                check_update<ALGO, MAXDC>(x, a.alpha);
+#pragma unroll
+                for (int s = 0; s < MAXDC; ++s)
+                    if (s < d) msg[s0 + s] = x[s];
+            }
+            __syncthreads();
+            int errs = 0;
+            for (int v = tid; v < n; v += T) {
+                const int e0 = a.vptr[v], e1 = a.vptr[v + 1];
+                float s = Ls[v];
+                for (int e = e0; e < e1; ++e) s += msg[a.vslot[e]];
+                for (int e = e0; e < e1; ++e) {
+                    const int sl = a.vslot[e];
+                    msg[sl] = s - msg[sl];
+                    if (ET) hs[sl] = (uint8_t)(s < 0.0f);
+                }
+                errs += (s < 0.0f);
+                if (!MC) {
+                    if (a.post) a.post[(size_t)b * n + v] = s;
+                    if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
+                }
+            }
+            if (MC) {
+                const int w = wave_sum(errs);
+                if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[it + 1], w);
+            }
+        }
+        __syncthreads();
+        if (MC) {
+            int32_t *tr = a.trial + (size_t)b * (iters + 1);
+            const int last = curve[it];
+            for (int i = tid; i <= iters; i += T) tr[i] = i <= it ? curve[i] : last;
+        }
+        if ((MC || a.its) && tid == 0) a.its[b] = it;
+    }
+}
+
+// ===========================================================================
+// 3. Stand-alone channel (rocRAND philox4x32_10 device API)
+// ===========================================================================
+__global__ __launch_bounds__(256) void channel_kernel(int kind, float p, float p2, uint64_t seed,
+                                                      uint64_t first_cw, int n, int B, void *out) {
+    const int groups = (n + 3) >> 2;
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)groups * B) return;
+    const int b = (int)(idx / groups), g = (int)(idx % groups);
+    rocrand_state_philox4x32_10 st;
+    rocrand_init(seed, first_cw + (uint64_t)b, 4ull * (uint64_t)g, &st);
+    const uint4 r = rocrand4(&st);
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    float val[4];
+    if (kind == 2) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float ua = u01(w[2 * h]), ub = u01(w[2 * h + 1]);
+            const float rad = sqrtf(-2.0f * logf(ua));
+            const float ang = 6.28318530717958647692f * ub;
+            val[2 * h] = (1.0f + p * (rad * cosf(ang))) * p2;
+            val[2 * h + 1] = (1.0f + p * (rad * sinf(ang))) * p2;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int v = 4 * g + i;
+        if (v >= n) break;
+        const size_t o = (size_t)b * n + v;
+        const float u = u01(w[i]);
+        if (kind == 0) static_cast<uint8_t *>(out)[o] = u < p ? 2 : 0;
+        else if (kind == 1) static_cast<float *>(out)[o] = u < p ? -p2 : p2;
+        else static_cast<float *>(out)[o] = val[i];
+    }
+}
+
+// ===========================================================================
+// 4. Monte-Carlo statistics: sequential stop rule + counter reduction
+// ===========================================================================
+// Trial b is a frame error when its final count f satisfies f > X && f != 0
+// (parallel_simulator_expurgated.py:238-243; X = -1 gives parallel_simulator.py:227-231).
+__global__ __launch_bounds__(1024) void mc_cutoff_kernel(const int32_t *trial, int B, int iters, int X,
+                                                         int64_t stop, const int64_t *counters,
+                                                         int32_t *cutoff) {
+    __shared__ int cnt[1024];
+    __shared__ int res;
+    const int tid = threadIdx.x;
+    if (stop <= 0) {
+        if (tid == 0) *cutoff = B;
+        return;
+    }
+    const int64_t remaining = stop - counters[1];
+    if (remaining <= 0) {
+        if (tid == 0) *cutoff = 0;
+        return;
+    }
+    const int chunk = (B + 1023) / 1024;
+    const int b0 = tid * chunk, b1 = min(B, b0 + chunk);
+    int c = 0;
+    for (int b = b0; b < b1; ++b) {
+        const int f = trial[(size_t)b * (iters + 1) + iters];
+        c += (f > X && f != 0);
+    }
+    cnt[tid] = c;
+    if (tid == 0) res = B;
+    __syncthreads();
+    if (tid == 0) {  // exclusive scan (1024 adds)
+        int acc = 0;
+        for (int i = 0; i < 1024; ++i) {
+            const int t = cnt[i];
+            cnt[i] = acc;
+            acc += t;
+        }
+    }
+    __syncthreads();
+    const int64_t before = cnt[tid];
+    if (before < remaining && before + c >= remaining) {
+        int64_t acc = before;
+        for (int b = b0; b < b1; ++b) {
+            const int f = trial[(size_t)b * (iters + 1) + iters];
+            acc += (f > X && f != 0);
+            if (acc >= remaining) {
+                res = b + 1;
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) *cutoff = res;
+}
+
+__global__ __launch_bounds__(256) void mc_reduce_kernel(const int32_t *trial, const int32_t *its, int B,
+                                                        int iters, int X, const int32_t *cutoff_p,
+                                                        int64_t *counters) {
+    __shared__ long long red[4][256 / kWave];
+    const int tid = threadIdx.x;
+    const int cutoff = min(B, *cutoff_p);
+    const int per = (B + gridDim.x - 1) / gridDim.x;
+    const int b0 = blockIdx.x * per, b1 = min(cutoff, b0 + per);
+    if (b0 >= b1) return;
+    // error curve columns, coalesced over t
+    for (int t = tid; t <= iters; t += 256) {
+        long long s = 0;
+        for (int b = b0; b < b1; ++b) {
+            const int32_t *row = trial + (size_t)b * (iters + 1);
+            if (row[iters] > X) s += row[t];
+        }
+        if (s) atomicAdd(reinterpret_cast<unsigned long long *>(counters + LDPC_MC_NCOUNT + t),
+                         (unsigned long long)s);
+    }
+    long long fr = 0, bits = 0, itn = 0;
+    for (int b = b0 + tid; b < b1; b += 256) {
+        const int f = trial[(size_t)b * (iters + 1) + iters];
+        if (f > X) {
+            fr += (f != 0);
+            bits += f;
+        }
+        itn += its[b];
+    }
+    long long v[3] = {fr, bits, itn};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        long long x = v[q];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
+        if ((tid & 63) == 0) red[q][tid / kWave] = x;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        long long s[3] = {0, 0, 0};
+        for (int q = 0; q < 3; ++q)
+            for (int w = 0; w < 256 / kWave; ++w) s[q] += red[q][w];
+        unsigned long long *c = reinterpret_cast<unsigned long long *>(counters);
+        atomicAdd(c + 0, (unsigned long long)(b1 - b0));
+        atomicAdd(c + 1, (unsigned long long)s[0]);
+        atomicAdd(c + 2, (unsigned long long)s[1]);
+        atomicAdd(c + 3, (unsigned long long)s[2]);
+    }
+}
+
+// ===========================================================================
+// Launch-side kernel selection
+// ===========================================================================
+constexpr size_t kLdsMax = 160 * 1024;
+
+template <typename K>
+hipError_t allow_lds(K kernel, size_t bytes) {
+    if (bytes <= 64 * 1024) return hipSuccess;
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+ChanArgs make_chan(int kind, float p, float p2, uint64_t seed) {
+    ChanArgs c;
+    c.kind = kind;
+    c.p = p;
+    c.p2 = p2;
+    c.k0 = (uint32_t)seed;
+    c.k1 = (uint32_t)(seed >> 32);
+    return c;
+}
+
+size_t bec_lds_bytes(const ldpc_graph &g, int iters) {
+    return (size_t)((iters * 4 + 15) & ~15) + (size_t)((g.n + 15) & ~15) + (size_t)g.m;
+}
+
+template <bool MC>
+hipError_t run_bec(const ldpc_graph &g, BecArgs a, int B, hipStream_t stream) {
+    const size_t lds = bec_lds_bytes(g, a.max_iters);
+    if (lds > kLdsMax - 1024) return hipErrorInvalidValue;
+    if (B <= 0) return hipSuccess;
+    if (g.n >= 4096) {
+        auto k = bec_kernel<1024, MC>;
+        hipError_t e = allow_lds(k, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3(B), dim3(1024), lds, stream, a);
+    } else {
+        auto k = bec_kernel<256, MC>;
+        hipError_t e = allow_lds(k, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3(B), dim3(256), lds, stream, a);
+    }
+    return hipGetLastError();
+}
+
+BecArgs bec_args(const ldpc_graph &g) {
+    BecArgs a{};
+    a.cvar = g.cvar;
+    a.cptr = g.cptr;
+    a.vptr = g.vptr;
+    a.vchk = g.vchk;
+    a.n = g.n;
+    a.m = g.m;
+    a.dv = g.dv;
+    a.dc = g.dc;
+    return a;
+}
+
+// --- soft path selection ---------------------------------------------------
+enum class BpPath { Lds36, Generic8, Generic16, Generic32, GenericG8, GenericG16, GenericG32, None };
+
+size_t lds36_bytes(const ldpc_graph &g, int iters, bool et, bool mc) {
+    size_t s = (size_t)g.E * 4;
+    if (et || mc) s = ((size_t)g.E * 5 + 15) & ~(size_t)15;
+    if (mc) s += (size_t)(iters + 1) * 4;
+    return s;
+}
+
+size_t generic_lds_bytes(const ldpc_graph &g, int iters, bool mc) {
+    return (((size_t)g.E * 5 + (size_t)g.n * 4 + 15) & ~(size_t)15) + (mc ? (size_t)(iters + 1) * 4 : 0);
+}
+
+BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc) {
+    if (!g.consistent) return BpPath::None;
+    if (g.dv == 3 && g.dc == 6 && g.n <= 13 * 1024 && lds36_bytes(g, iters, et, mc) <= kLdsMax - 2048)
+        return BpPath::Lds36;
+    const int d = g.max_cdeg;
+    if (d > 32) return BpPath::None;
+    const bool lds = generic_lds_bytes(g, iters, mc) <= kLdsMax - 2048;
+    if (d <= 8) return lds ? BpPath::Generic8 : BpPath::GenericG8;
+    if (d <= 16) return lds ? BpPath::Generic16 : BpPath::GenericG16;
+    return lds ? BpPath::Generic32 : BpPath::GenericG32;
+}
+
+template <int VPT, int T, int ALGO, bool ET, bool MC>
+hipError_t launch_lds36_vpt(const ldpc_graph &g, BpArgs a, size_t lds, hipStream_t s) {
+    auto k = bp_lds_kernel<3, 6, T, VPT, ALGO, ET, MC>;
+    hipError_t e = allow_lds(k, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(a.B), dim3(T), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int ALGO, bool ET, bool MC>
+hipError_t launch_lds36(const ldpc_graph &g, BpArgs a, hipStream_t s) {
+    const size_t lds = lds36_bytes(g, a.max_iters, ET, MC);
+    if (g.n <= 256) return launch_lds36_vpt<1, 256, ALGO, ET, MC>(g, a, lds, s);
+    if (g.n <= 512) return launch_lds36_vpt<2, 256, ALGO, ET, MC>(g, a, lds, s);
+    if (g.n <= 1024) return launch_lds36_vpt<4, 256, ALGO, ET, MC>(g, a, lds, s);
+    if (g.n <= 2048) return launch_lds36_vpt<8, 256, ALGO, ET, MC>(g, a, lds, s);
+    if (g.n <= 4 * 1024) return launch_lds36_vpt<4, 1024, ALGO, ET, MC>(g, a, lds, s);
+    if (g.n <= 8 * 1024) return launch_lds36_vpt<8, 1024, ALGO, ET, MC>(g, a, lds, s);
+    if (g.n <= 10 * 1024) return launch_lds36_vpt<10, 1024, ALGO, ET, MC>(g, a, lds, s);
+    return launch_lds36_vpt<13, 1024, ALGO, ET, MC>(g, a, lds, s);
+}
+
+template <int MAXDC, int ALGO, bool ET, bool MC, bool GMEM>
+hipError_t launch_generic(const ldpc_graph &g, BpArgs a, hipStream_t s) {
+    constexpr int T = 256;
+    auto k = bp_generic_kernel<T, MAXDC, ALGO, ET, MC, GMEM>;
+    const size_t lds = GMEM ? (MC ? (size_t)(a.max_iters + 1) * 4 : 0) : generic_lds_bytes(g, a.max_iters, MC);
+    hipError_t e = allow_lds(k, lds);
+    if (e != hipSuccess) return e;
+    int grid = a.B;
+    if (GMEM) grid = a.B < 2048 ? a.B : 2048;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int ALGO, bool ET, bool MC>
+hipError_t dispatch_bp(const ldpc_graph &g, BpArgs a, hipStream_t s) {
+    switch (choose_path(g, a.max_iters, ET, MC)) {
+        case BpPath::Lds36: return launch_lds36<ALGO, ET, MC>(g, a, s);
+        case BpPath::Generic8: return launch_generic<8, ALGO, ET, MC, false>(g, a, s);
+        case BpPath::Generic16: return launch_generic<16, ALGO, ET, MC, false>(g, a, s);
+        case BpPath::Generic32: return launch_generic<32, ALGO, ET, MC, false>(g, a, s);
+        case BpPath::GenericG8: return launch_generic<8, ALGO, ET, MC, true>(g, a, s);
+        case BpPath::GenericG16: return launch_generic<16, ALGO, ET, MC, true>(g, a, s);
+        case BpPath::GenericG32: return launch_generic<32, ALGO, ET, MC, true>(g, a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <bool MC>
+hipError_t dispatch_bp_algo(const ldpc_graph &g, BpArgs a, int algo, int et, hipStream_t s) {
+    if (algo == 0) return et ? dispatch_bp<0, true, MC>(g, a, s) : dispatch_bp<0, false, MC>(g, a, s);
+    return et ? dispatch_bp<1, true, MC>(g, a, s) : dispatch_bp<1, false, MC>(g, a, s);
+}
+
+BpArgs bp_args(const ldpc_graph &g, int B, int iters, float alpha) {
+    BpArgs a{};
+    a.cptr = g.cptr;
+    a.cvar = g.cvar;
+    a.vptr = g.vptr;
+    a.vslot = g.vslot;
+    a.n = g.n;
+    a.m = g.m;
+    a.E = g.E;
+    a.B = B;
+    a.max_iters = iters;
+    a.alpha = alpha;
+    return a;
+}
+
+}  // namespace
+
+// ===========================================================================
+// Launchers (ldpc_internal.hpp)
+// ===========================================================================
+hipError_t launch_bec_decode(const ldpc_graph &g, uint8_t *d_words, int B, int max_iters,
+                             int32_t *d_errors, int32_t *d_its, hipStream_t stream) {
+    BecArgs a = bec_args(g);
+    a.words = d_words;
+    a.errors = d_errors;
+    a.its = d_its;
+    a.max_iters = max_iters;
+    return run_bec<false>(g, a, B, stream);
+}
+
+size_t bp_scratch_bytes(const ldpc_graph &g, int B) {
+    const size_t per = ((size_t)g.E * 5 + (size_t)g.n * 4 + 15) & ~(size_t)15;
+    if (generic_lds_bytes(g, 0, true) + 4096 <= kLdsMax) return 0;
+    const int grid = B < 2048 ? B : 2048;
+    return per * (size_t)grid;
+}
+
+const char *bp_kernel_name(const ldpc_graph &g, int early_stop) {
+    switch (choose_path(g, 50, early_stop != 0, false)) {
+        case BpPath::Lds36: return "bp_lds_kernel<3,6>";
+        case BpPath::Generic8: return "bp_generic_kernel<8,lds>";
+        case BpPath::Generic16: return "bp_generic_kernel<16,lds>";
+        case BpPath::Generic32: return "bp_generic_kernel<32,lds>";
+        case BpPath::GenericG8: return "bp_generic_kernel<8,gmem>";
+        case BpPath::GenericG16: return "bp_generic_kernel<16,gmem>";
+        case BpPath::GenericG32: return "bp_generic_kernel<32,gmem>";
+        default: return "none";
+    }
+}
+
+hipError_t launch_bp_decode(const ldpc_graph &g, const float *d_llr, int B, int max_iters, int algo,
+                            float alpha, int early_stop, float *d_post, uint8_t *d_hard,
+                            int32_t *d_its, hipStream_t stream, float *d_scratch) {
+    if (B <= 0) return hipSuccess;
+    BpArgs a = bp_args(g, B, max_iters, alpha);
+    a.llr = d_llr;
+    a.post = d_post;
+    a.hard = d_hard;
+    a.its = d_its;
+    a.scratch = d_scratch;
+    return dispatch_bp_algo<false>(g, a, algo, early_stop, stream);
+}
+
+hipError_t launch_channel(int channel, float p, float p2, uint64_t seed, uint64_t first_cw, int n, int B,
+                          void *d_out, hipStream_t stream) {
+    if (B <= 0 || n <= 0) return hipSuccess;
+    const size_t total = (size_t)((n + 3) / 4) * (size_t)B;
+    const unsigned grid = (unsigned)((total + 255) / 256);
+    hipLaunchKernelGGL(channel_kernel, dim3(grid), dim3(256), 0, stream, channel, p, p2, seed, first_cw, n, B,
+                       d_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_mc_decode(const ldpc_graph &g, int channel, float p, float p2, uint64_t seed,
+                            uint64_t first_cw, int B, int max_iters, int algo, float alpha, int early_stop,
+                            int32_t *trial, int32_t *trial_its, hipStream_t stream, float *d_scratch) {
+    if (B <= 0) return hipSuccess;
+    if (channel == 0) {
+        BecArgs a = bec_args(g);
+        a.max_iters = max_iters;
+        a.ch = make_chan(channel, p, p2, seed);
+        a.first_cw = first_cw;
+        a.trial = trial;
+        a.its = trial_its;
+        return run_bec<true>(g, a, B, stream);
+    }
+    BpArgs a = bp_args(g, B, max_iters, alpha);
+    a.ch = make_chan(channel, p, p2, seed);
+    a.first_cw = first_cw;
+    a.trial = trial;
+    a.its = trial_its;
+    a.scratch = d_scratch;
+    return dispatch_bp_algo<true>(g, a, algo, early_stop, stream);
+}
+
+hipError_t launch_mc_reduce(const int32_t *trial, const int32_t *trial_its, int B, int max_iters,
+                            int expurgation, int64_t stop_frame_errors, int64_t *d_counters,
+                            int32_t *d_cutoff, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mc_cutoff_kernel, dim3(1), dim3(1024), 0, stream, trial, B, max_iters, expurgation,
+                       stop_frame_errors, d_counters, d_cutoff);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int blocks = B < 1024 ? (B + 63) / 64 : 256;
+    hipLaunchKernelGGL(mc_reduce_kernel, dim3(blocks), dim3(256), 0, stream, trial, trial_its, B, max_iters,
+                       expurgation, d_cutoff, d_counters);
+    return hipGetLastError();
+}
+
+}  // namespace ldpc

@@ -1,0 +1,162 @@
+/*
+ * ldpc_mi355x.h -- C ABI of libldpc_mi355x.so, the MI355X (gfx950) LDPC
+ * belief-propagation engine.
+ *
+ * Plain C types only (pointers + sizes); no torch / HIP types in signatures.
+ * `stream` arguments are hipStream_t passed as void* (NULL = default stream).
+ *
+ * Every entry point cites the reference interface it replaces or extends
+ * (paths relative to roryhighnam/iib_project_ldpc_codes).
+ *
+ * Return convention for the new entry points: 0 = OK, negative = error
+ * (LDPC_E*); ldpc_last_error() returns a human-readable message.  The drop-in
+ * message_passing keeps the reference's convention (returns the iteration
+ * index) and returns a negative LDPC_E* code on failure.
+ */
+#ifndef LDPC_MI355X_H
+#define LDPC_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDPC_OK 0
+#define LDPC_EINVAL (-1)  /* bad argument / inconsistent graph / value outside {0,1,2} */
+#define LDPC_ENODEV (-2)  /* no MI355X visible / HIP runtime error at init */
+#define LDPC_EHIP (-3)    /* HIP runtime error during a call */
+#define LDPC_ENOMEM (-4)
+#define LDPC_EUNSUP (-5)  /* configuration not supported by any kernel */
+
+/* Channels (channels.py:4-26 BEC; BSC and BI-AWGN are new). */
+#define LDPC_CH_BEC 0   /* param = erasure probability                          */
+#define LDPC_CH_BSC 1   /* param = crossover probability                        */
+#define LDPC_CH_AWGN 2  /* param = noise std-dev sigma (BPSK +-1, LLR = 2y/s^2)  */
+
+/* Soft decoding algorithms (no reference counterpart). */
+#define LDPC_ALGO_SPA 0      /* sum-product, tanh rule, fp32                     */
+#define LDPC_ALGO_MINSUM 1   /* normalized min-sum (alpha), fp32                 */
+
+/* ---------------------------------------------------------------------- */
+/* Drop-in                                                                 */
+/* ---------------------------------------------------------------------- */
+/*
+ * Replaces message_passing.c:7 (`int message_passing(int *Mvc, int iterations,
+ * int *variable_to_check_list, int *check_to_variable_list, int *errors, int n,
+ * int k, int dv, int dc)`), bound by ctypes at parallel_simulator.py:162-164
+ * and parallel_simulator_expurgated.py:162-164.  Same symbol, arguments and
+ * semantics: Mvc (0/1/2, int32[n]) decoded in place, errors[it] += erasure
+ * count per iteration (caller zeroes it), stall skip, returns the break
+ * iteration or `iterations`.  Runs one codeword on the current HIP device.
+ */
+int message_passing(int *Mvc, int iterations, int *variable_to_check_list,
+                    int *check_to_variable_list, int *errors, int n, int k, int dv, int dc);
+
+/* ---------------------------------------------------------------------- */
+/* Tanner graph handle                                                     */
+/* ---------------------------------------------------------------------- */
+typedef struct ldpc_graph ldpc_graph;
+
+/*
+ * Upload a regular graph given in the reference's edge-list format
+ * (random_code_generator.c:34-36 check_lookup = check_to_variable_list,
+ * int32[(n-k)*dc]; random_code_generator.c:57-62 variable_lookup =
+ * variable_to_check_list, int32[n*dv]) to the current device.
+ */
+int ldpc_graph_create(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list,
+                      int n, int k, int dv, int dc, ldpc_graph **out);
+
+/*
+ * Upload an irregular graph in CSR slot form (new):
+ * check c owns slots [check_ptr[c], check_ptr[c+1]) with check_var[slot] its
+ * variable; variable v owns edges [var_ptr[v], var_ptr[v+1]) with var_slot[]
+ * naming the slot of each edge.
+ */
+int ldpc_graph_create_csr(const int32_t *check_ptr, const int32_t *check_var, const int32_t *var_ptr,
+                          const int32_t *var_slot, int n, int m, ldpc_graph **out);
+
+void ldpc_graph_destroy(ldpc_graph *g);
+int ldpc_graph_info(const ldpc_graph *g, int32_t *n, int32_t *m, int32_t *num_edges);
+
+/* ---------------------------------------------------------------------- */
+/* Batched BEC erasure decoding (message_passing.c:7-82 over B words)     */
+/* ---------------------------------------------------------------------- */
+/*
+ * Host-pointer form: words uint8[B*n] (0/1/2, in/out),
+ * errors int32[B*max_iters] (accumulated, as message_passing.c:73),
+ * its int32[B] (return value of each message_passing call).
+ */
+int ldpc_bec_decode_batch(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list,
+                          int n, int k, int dv, int dc, uint8_t *words, int B, int max_iters,
+                          int32_t *errors, int32_t *its);
+
+/* Device-pointer form on a prepared graph; asynchronous on `stream`. */
+int ldpc_bec_decode_batch_dev(const ldpc_graph *g, uint8_t *d_words, int B, int max_iters,
+                              int32_t *d_errors, int32_t *d_its, void *stream);
+
+/* ---------------------------------------------------------------------- */
+/* Batched soft decoding (new: SURVEY.md 8b-3)                            */
+/* ---------------------------------------------------------------------- */
+/*
+ * llr float[B*n] channel LLRs (log P(0)/P(1)); outputs posterior LLRs
+ * post float[B*n] (may be NULL), hard decisions hard uint8[B*n] (may be NULL,
+ * 1 where post < 0) and iterations run its int32[B] (may be NULL).
+ * early_stop != 0 stops a codeword once its hard decision satisfies every check.
+ */
+int ldpc_bp_decode_batch(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list,
+                         int n, int k, int dv, int dc, const float *llr, int B, int max_iters,
+                         int algo, float alpha, int early_stop, float *post, uint8_t *hard,
+                         int32_t *its);
+
+int ldpc_bp_decode_batch_dev(const ldpc_graph *g, const float *d_llr, int B, int max_iters, int algo,
+                             float alpha, int early_stop, float *d_post, uint8_t *d_hard,
+                             int32_t *d_its, void *stream);
+
+/* ---------------------------------------------------------------------- */
+/* On-device channels (channels.py:24-26 new_transmit + BSC / BI-AWGN)     */
+/* ---------------------------------------------------------------------- */
+/*
+ * Channel outputs for the all-zero codeword (parallel_simulator.py:222) of
+ * codewords first_cw .. first_cw+B-1, Philox4x32-10 (rocRAND) keyed by seed:
+ * BEC writes uint8 0/2 into d_out, BSC / AWGN write float LLRs.
+ */
+int ldpc_channel_dev(int channel, float param, uint64_t seed, uint64_t first_cw, int n, int B,
+                     void *d_out, void *stream);
+
+/* ---------------------------------------------------------------------- */
+/* Monte-Carlo batch (run_simulation trial loop, parallel_simulator.py:198-244) */
+/* ---------------------------------------------------------------------- */
+/*
+ * One fused device batch: B trials first_cw .. first_cw+B-1: channel ->
+ * decode -> per-trial statistics.  counters int64[LDPC_MC_NCOUNT + max_iters + 1]
+ * on the device, ACCUMULATED (+=):
+ *   [0] trials  [1] frame errors  [2] bit errors (residual erasures / wrong bits)
+ *   [3] decoding iterations executed  [4..] error curve[0..max_iters]
+ *   (BEC: erasures before decoding and after each iteration -- the
+ *    `errors` vector of parallel_simulator.py:165 summed as at :227;
+ *    soft: wrong hard decisions after each iteration, [4] = channel errors).
+ * A trial counts only when its final error count is > expurgation
+ * (parallel_simulator_expurgated.py:238); pass -1 for the plain simulator.
+ * If stop_frame_errors > 0 the batch honours the sequential stop rule
+ * (parallel_simulator.py:198): only trials up to and including the one that
+ * brings counters[1] to stop_frame_errors are counted.
+ * algo is ignored for BEC (exact erasure decoding, message_passing.c).
+ */
+#define LDPC_MC_NCOUNT 4
+int ldpc_mc_batch_dev(const ldpc_graph *g, int channel, float param, uint64_t seed, uint64_t first_cw,
+                      int B, int max_iters, int algo, float alpha, int early_stop, int expurgation,
+                      int64_t stop_frame_errors, int64_t *d_counters, void *stream);
+
+/* ---------------------------------------------------------------------- */
+/* Misc                                                                    */
+/* ---------------------------------------------------------------------- */
+const char *ldpc_last_error(void);
+int ldpc_device_count(void);
+int ldpc_set_device(int device);
+int ldpc_sync(void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDPC_MI355X_H */

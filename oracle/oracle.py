@@ -44,6 +44,8 @@ def lib():
         _lib.oracle_channel.restype = None
         _lib.oracle_density_evolution.argtypes = [ct.c_double, i, i, i, ct.c_double, P]
         _lib.oracle_density_evolution.restype = i
+        _lib.oracle_num_threads.argtypes = []
+        _lib.oracle_num_threads.restype = i
     return _lib
 
 
@@ -100,6 +102,10 @@ def bp_decode_batch(csr, llr, max_iters, algo=0, alpha=1.0, early_stop=False):
     lib().oracle_bp_decode_batch(_p(cptr), _p(cvar), _p(vptr), _p(vslot), n, m, _p(llr), B, max_iters,
                                  algo, alpha, int(bool(early_stop)), _p(post), _p(hard), _p(its))
     return post, hard, its
+
+
+def num_threads():
+    return int(lib().oracle_num_threads())
 
 
 def philox(ctr, key):

@@ -1,0 +1,131 @@
+"""CPU-side tests: the C-ABI library loads and exports every declared symbol, fails loudly
+without a GPU, and the host logic (graph sampler, list <-> CSR, CLI surface) is right."""
+import ctypes as ct
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _torch_has_gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def test_library_exports_every_header_symbol():
+    from iib_project_ldpc_codes_amd import _native
+    L = _native.lib()
+    hdr = open(os.path.join(ROOT, "include", "ldpc_mi355x.h")).read()
+    declared = set(re.findall(r"^(?:int|void|const char \*)\s*\**(\w+)\(", hdr, re.M))
+    assert {"message_passing", "ldpc_bp_decode_batch_dev", "ldpc_mc_batch_dev"} <= declared
+    for name in declared:
+        assert hasattr(L, name), name
+    for name in _native.exported_symbols():
+        assert name in declared
+
+
+@pytest.mark.skipif(_torch_has_gpu(), reason="checks the no-GPU failure mode")
+def test_no_gpu_fails_loudly():
+    from iib_project_ldpc_codes_amd import _native
+    L = _native.lib()
+    assert L.ldpc_device_count() == 0
+    w = np.zeros(12, np.int32)
+    w[3] = 2
+    e = np.zeros(5, np.int32)
+    v2c = np.zeros(36, np.int32)
+    c2v = np.zeros(36, np.int32)
+    rc = L.message_passing(w.ctypes.data, 5, v2c.ctypes.data, c2v.ctypes.data, e.ctypes.data, 12, 6, 3, 6)
+    assert rc == _native.LDPC_ENODEV
+    assert "no HIP device" in _native.last_error()
+
+
+def test_random_regular_law():
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = TannerGraph.random_regular(1000, 3, 6, seed=5)
+    assert g.m == 500 and g.check_lookup.size == 3000
+    rows = g.check_lookup.reshape(500, 6)
+    assert all(len(set(r)) == 6 for r in rows)  # no repeated variable in a check
+    assert np.all(np.bincount(g.check_lookup, minlength=1000) == 3)
+    v = g.variable_lookup.reshape(1000, 3)
+    assert np.all(np.diff(v, axis=1) > 0)  # ascending, as random_code_generator.c:57-62
+    # lists agree with each other
+    H = g.parity_check()
+    assert np.all(H.sum(0) == 3) and np.all(H.sum(1) == 6)
+    for var in range(0, 1000, 97):
+        assert set(np.nonzero(H[:, var])[0]) == set(v[var])
+
+
+def test_to_csr_matches_oracle():
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = TannerGraph.random_regular(300, 3, 6, seed=9)
+    mine = g.to_csr()
+    ref = oracle.csr_from_lists(g.variable_lookup, g.check_lookup, g.n, g.m, 3, 6)
+    for a, b in zip(mine, ref):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_from_parity_check_roundtrip():
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = TannerGraph.random_regular(60, 3, 6, seed=2)
+    h = TannerGraph.from_parity_check(g.parity_check())
+    np.testing.assert_array_equal(h.variable_lookup, g.variable_lookup)
+    np.testing.assert_array_equal(np.sort(h.check_lookup.reshape(30, 6), 1), np.sort(g.check_lookup.reshape(30, 6), 1))
+
+
+def test_reference_generator_law_matches_ours():
+    """The reference generator (random_code_generator.c via oracle/_ref) and ours draw from the same
+    configuration-model law: compare the distribution of a graph statistic (number of
+    length-4 cycles) over many small graphs."""
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built")
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+
+    def c4(H):
+        O = H.astype(np.int64) @ H.T.astype(np.int64)
+        np.fill_diagonal(O, 0)
+        return int((O * (O - 1) // 2).sum() // 2)
+
+    ref = [c4(oracle.ref_generate_random_code(40, 3, 6)[2].astype(np.uint8)) for _ in range(300)]
+    ours = [c4(TannerGraph.random_regular(40, 3, 6, seed=s).parity_check()) for s in range(300)]
+    assert abs(np.mean(ref) - np.mean(ours)) < 4 * np.sqrt((np.var(ref) + np.var(ours)) / 300)
+
+
+def test_channel_params_match_kernel_contract():
+    assert oracle.channel_params(oracle.CH_BSC, 0.1)[1] == pytest.approx(np.log(9), rel=1e-6)
+    assert oracle.channel_params(oracle.CH_AWGN, 0.5)[1] == pytest.approx(8.0)
+
+
+def test_bec_oracle_channel_law():
+    x = oracle.channel(oracle.CH_BEC, 0.4, 7, 0, 1000, 200)
+    assert abs((x == 2).mean() - 0.4) < 0.005
+    y = oracle.channel(oracle.CH_AWGN, 1.0, 7, 0, 1000, 100) / 2.0
+    assert abs(y.mean() - 1.0) < 0.01 and abs(y.std() - 1.0) < 0.01
+
+
+def test_cli_surface_parses(monkeypatch):
+    from iib_project_ldpc_codes_amd import parallel_simulator as ps
+    seen = {}
+    monkeypatch.setattr(ps, "run_simulation", lambda d: seen.setdefault("ens", d))
+    monkeypatch.setattr(ps, "run_simulation_fixed_ldpc", lambda d: seen.setdefault("fixed", d))
+    ps.main(["0.4", "100", "50", "1000", "3", "6", "0", "7"])
+    ps.main(["0.4", "100", "50", "1000", "3", "6", "3", "2"])
+    assert seen["ens"]["seed"] == 7 and seen["ens"]["message_passing"] and not seen["ens"]["optimal"]
+    assert seen["fixed"]["filenumber"] == 2
+    with pytest.raises(ValueError):
+        ps.main(["0.4", "100", "50", "1000", "3", "6", "9", "7"])
+
+
+def test_csv_writer_format(tmp_path, monkeypatch):
+    from iib_project_ldpc_codes_amd import parallel_simulator as ps
+    monkeypatch.setattr(ps, "base_directory", str(tmp_path) + os.sep)
+    ps.write_message_passing_file("x.csv", [0.4, 0.3], 0.1, 0.02)
+    txt = open(tmp_path / "report_data" / "simulation_data" / "x.csv").read().splitlines()
+    assert txt == ["0.4", "0.3", "Message passing block-wise error,0.1", "Message passing bit-wise error,0.02"]

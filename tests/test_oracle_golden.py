@@ -6,22 +6,13 @@ import numpy as np
 import pytest
 
 from oracle import oracle
+from tests.golden_util import load_bec_golden
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
 def _load():
-    z = np.load(os.path.join(GOLD, "bec_golden.npz"))
-    graphs = {}
-    for gi in range(int(z["num_graphs"][0])):
-        n, k, dv, dc = map(int, z[f"g{gi}_n"])
-        graphs[gi] = (n, k, dv, dc, z[f"g{gi}_v2c"], z[f"g{gi}_c2v"])
-    cases = []
-    for ci in range(int(z["num_cases"][0])):
-        gi, max_its, it, has_err = map(int, z[f"c{ci}_meta"])
-        cases.append(dict(gi=gi, max_its=max_its, it=it, word=z[f"c{ci}_word"], out=z[f"c{ci}_out"],
-                          errors=z[f"c{ci}_errors"], errin=z[f"c{ci}_errin"] if has_err else None))
-    return graphs, cases
+    return load_bec_golden()
 
 
 GRAPHS, CASES = _load()
