@@ -1,0 +1,28 @@
+#!/bin/bash
+# GPU box: kernel-trace stats of the bench command + PMC passes (one counter group per pass).
+#   TAG=r01 ./scripts/profile.sh
+set -u
+TAG=${TAG:-r01}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+BENCH="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 $BENCH > $OUT/trace_bench.log 2>&1 || exit $?
+echo "trace ok"; tail -1 $OUT/trace_bench.log
+PMCB="bench.py --steps 1 --warmup 0 --batch ${PMC_BATCH:-16384} --no-cpu-baseline --no-extras"
+i=0
+while read -r grp; do
+  [ -z "$grp" ] && continue
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "${KREGEX:-bp_lds}" -f csv -d $OUT/pmc$i -o run -- python3 $PMCB > $OUT/pmc$i.log 2>&1
+  rc=$?
+  echo "pmc pass $i ($grp) rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 $OUT/pmc$i.log; [ $rc -ge 124 ] && exit $rc; fi
+done <<GROUPS
+${PMC_GROUPS:-FETCH_SIZE
+WRITE_SIZE
+SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS
+SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT}
+GROUPS
+exit 0
