@@ -8,6 +8,8 @@
 //   parallel_simulator.py:198-244  -> mc_* (per-trial statistics + stop rule)
 #include <rocrand/rocrand_kernel.h>
 
+#include <type_traits>
+
 #include "ldpc_internal.hpp"
 #include "ldpc_mi355x.h"
 
@@ -206,15 +208,18 @@ __global__ __launch_bounds__(T) void bec_kernel(BecArgs a) {
 // ===========================================================================
 // 2. Soft flooding BP (no reference counterpart; oracle_bp_decode defines it)
 // ===========================================================================
+// Raw CDNA transcendentals (v_exp_f32 = 2^x, v_log_f32 = log2, v_rcp_f32; ~1 ulp):
+// ~7 VALU per conversion instead of the IEEE division / range-reduced libm paths.
 __device__ __forceinline__ float tanh_half(float x) {
-    const float e = __expf(-fabsf(x));
-    const float t = __fdividef(1.0f - e, 1.0f + e);
-    return x < 0.0f ? -t : t;
+    const float e = __builtin_amdgcn_exp2f(fabsf(x) * -1.44269504088896341f);  // exp(-|x|)
+    const float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
+    return copysignf(t, x);
 }
 
 __device__ __forceinline__ float atanh2(float p) {
-    p = fminf(fmaxf(p, -kPMax), kPMax);
-    return __logf(__fdividef(1.0f + p, 1.0f - p));
+    p = __builtin_amdgcn_fmed3f(p, -kPMax, kPMax);
+    const float r = (1.0f + p) * __builtin_amdgcn_rcpf(1.0f - p);
+    return __builtin_amdgcn_logf(r) * 0.693147180559945309f;
 }
 
 // Check-node update over D messages in registers (padding: +inf, neutral for
@@ -283,8 +288,12 @@ template <int DV, int DC, int T, int VPT, int ALGO, bool ET, bool MC>
 __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     float *msg = reinterpret_cast<float *>(smem);
-    uint8_t *hs = smem + (size_t)a.E * 4;
-    int *curve = reinterpret_cast<int *>(smem + (((size_t)a.E * 5 + 15) & ~(size_t)15));
+    // DV dummy slots after the E real ones absorb the gathers of the padded
+    // variables v >= n (L = 0, messages stay 0), so the variable phase needs no
+    // per-variable guard.
+    const int Ep = a.E + 4;
+    uint8_t *hs = smem + (size_t)Ep * 4;
+    int *curve = reinterpret_cast<int *>(smem + (((size_t)Ep * 5 + 15) & ~(size_t)15));
     const int tid = threadIdx.x;
     const int n = a.n, m = a.m, iters = a.max_iters;
     constexpr int NS = VPT * DV;            // slots owned through my variables
@@ -306,11 +315,12 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             if (v < n) {
                 L[i] = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
                 err0 += (L[i] < 0.0f);
+            }
 #pragma unroll
-                for (int j = 0; j < DV; ++j) {
-                    const int q = i * DV + j;
-                    sp[q >> 1] |= (uint32_t)a.vslot[v * DV + j] << (16 * (q & 1));
-                }
+            for (int j = 0; j < DV; ++j) {
+                const int q = i * DV + j;
+                const int slot = v < n ? a.vslot[v * DV + j] : a.E + j;
+                sp[q >> 1] |= (uint32_t)slot << (16 * (q & 1));
             }
             if constexpr (KEEP_POST) pr[i] = L[i];
         }
@@ -321,10 +331,8 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < VPT; ++i) {
-            if (tid + i * T < n) {
 #pragma unroll
-                for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = L[i];
-            }
+            for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = L[i];
         }
         __syncthreads();
         if (MC) {
@@ -342,6 +350,45 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             }
         }
 
+        // the last fixed-count iteration writes the outputs instead of
+        // extrinsic messages; two straight-line copies keep the gathers free
+        // of per-variable branches.
+        auto var_phase = [&](auto final_tag) {
+            constexpr bool FINAL = decltype(final_tag)::value;
+            int errs = 0;
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) {
+                const int v = tid + i * T;
+                {
+                    float cv[DV];
+                    float s = L[i];
+#pragma unroll
+                    for (int j = 0; j < DV; ++j) {
+                        cv[j] = msg[SLOT(i, j)];
+                        s += cv[j];
+                    }
+                    if constexpr (FINAL) {
+                        if (v < n) {
+                            if (a.post) a.post[(size_t)b * n + v] = s;
+                            if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
+                        }
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = s - cv[j];
+                    }
+                    if constexpr (KEEP_POST) pr[i] = s;
+                    if constexpr (ET) {
+#pragma unroll
+                        for (int j = 0; j < DV; ++j) hs[SLOT(i, j)] = (uint8_t)(s < 0.0f);
+                    }
+                    if constexpr (MC) errs += (v < n) & (s < 0.0f);
+                }
+                // at most two variables' gathers in flight per thread (VGPR
+                // budget of 4 waves/SIMD; the 16 waves of the CU hide LDS latency)
+                if (i & 1) __builtin_amdgcn_sched_barrier(0);
+            }
+            return errs;
+        };
         int it = 0;
         for (; it < iters; ++it) {
             if (ET && it > 0) {  // syndrome of the previous iteration's hard decision
@@ -387,41 +434,20 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             // VPT*DV unpacked addresses in VGPRs and spill).
 #pragma unroll
             for (int q = 0; q < (NS + 1) / 2; ++q) asm volatile("" : "+v"(sp[q]));
-            const bool final_it = !ET && !MC && it == iters - 1;
-            int errs = 0;
-#pragma unroll
-            for (int i = 0; i < VPT; ++i) {
-                const int v = tid + i * T;
-                if (v < n) {
-                    float cv[DV];
-                    float s = L[i];
-#pragma unroll
-                    for (int j = 0; j < DV; ++j) {
-                        cv[j] = msg[SLOT(i, j)];
-                        s += cv[j];
-                    }
-                    if (final_it) {
-                        if (a.post) a.post[(size_t)b * n + v] = s;
-                        if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = s - cv[j];
-                    }
-                    if constexpr (KEEP_POST) pr[i] = s;
-                    if (ET) {
-#pragma unroll
-                        for (int j = 0; j < DV; ++j) hs[SLOT(i, j)] = (uint8_t)(s < 0.0f);
-                    }
-                    errs += (s < 0.0f);
-                }
-                // keep at most two variables' gathers in flight per thread:
-                // bounds VGPRs at 4 waves/SIMD (16 waves/CU hide the LDS latency)
-                if (i & 1) __builtin_amdgcn_sched_barrier(0);
-            }
+            // fixed-count decode: the last variable phase runs after the loop and
+            // writes the outputs (keeps its 64-bit output addresses out of the loop)
+            if (!ET && !MC && it == iters - 1) break;
+            const int errs = var_phase(std::false_type{});
             if (MC) {
                 const int w = wave_sum(errs);
                 if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[it + 1], w);
             }
+        }
+        if (!ET && !MC && iters > 0) {
+#pragma unroll
+            for (int q = 0; q < (NS + 1) / 2; ++q) asm volatile("" : "+v"(sp[q]));
+            (void)var_phase(std::true_type{});
+            it = iters;
         }
 #undef SLOT
         if (MC) {
@@ -746,8 +772,9 @@ BecArgs bec_args(const ldpc_graph &g) {
 enum class BpPath { Lds36, Generic8, Generic16, Generic32, GenericG8, GenericG16, GenericG32, None };
 
 size_t lds36_bytes(const ldpc_graph &g, int iters, bool et, bool mc) {
-    size_t s = (size_t)g.E * 4;
-    if (et || mc) s = ((size_t)g.E * 5 + 15) & ~(size_t)15;
+    const size_t Ep = (size_t)g.E + 4;
+    size_t s = Ep * 4;
+    if (et || mc) s = (Ep * 5 + 15) & ~(size_t)15;
     if (mc) s += (size_t)(iters + 1) * 4;
     return s;
 }
