@@ -63,6 +63,7 @@ def lib():
         "ldpc_set_device": ([i], i),
         "ldpc_sync": ([P], i),
         "ldpc_bp_kernel_name": ([P, i], ct.c_char_p),
+        "ldpc_debug_lane_layout": ([P, P, i, i, i, i, P, P, P, P], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -87,4 +88,4 @@ def exported_symbols():
     return ["message_passing", "ldpc_graph_create", "ldpc_graph_create_csr", "ldpc_graph_destroy",
             "ldpc_graph_info", "ldpc_bec_decode_batch", "ldpc_bec_decode_batch_dev", "ldpc_bp_decode_batch",
             "ldpc_bp_decode_batch_dev", "ldpc_channel_dev", "ldpc_mc_batch_dev", "ldpc_last_error",
-            "ldpc_device_count", "ldpc_set_device", "ldpc_sync"]
+            "ldpc_device_count", "ldpc_set_device", "ldpc_sync", "ldpc_debug_lane_layout", "ldpc_bp_kernel_name"]

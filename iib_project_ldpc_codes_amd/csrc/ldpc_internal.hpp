@@ -22,7 +22,32 @@ struct ldpc_graph {
                                  //       that check holds v != 1 times (never assigns)
     int32_t *vslot = nullptr;    // [E]   soft: slot of each variable edge (consistent only)
     int vchk_len = 0;
+    // Conflict-aware lane layout of the LDS-resident (3,6) kernel (see
+    // build_lane_layout in capi.cpp): position p = t + i*T is thread t's i-th
+    // variable; every 32 consecutive positions form one half-wave LDS access.
+    int lane_T = 0, lane_VPT = 0;
+    int32_t *lane_var = nullptr;   // [T*VPT]    variable id, -1 = padding lane
+    int32_t *lane_slot = nullptr;  // [T*VPT*dv] slot per edge (padding lanes: dummy slots >= E)
 };
+
+// Threads per workgroup and variables per thread of the LDS-resident kernel
+// for block length n: >= 3 % spare lanes so the layout can avoid LDS bank
+// conflicts.  Must match the instantiations in ldpc_kernels.hip.
+inline bool lds_shape(int n, int &T, int &VPT) {
+    static const int v256[] = {1, 2, 3, 5, 9};
+    static const int v1024[] = {2, 3, 5, 6, 9, 11, 14};
+    const long need = ((long)n * 103 + 99) / 100;
+    if (n <= 2048) {
+        T = 256;
+        for (int v : v256)
+            if (256L * v >= need) { VPT = v; return true; }
+    }
+    T = 1024;
+    for (int v : v1024)
+        if (1024L * v >= need) { VPT = v; return true; }
+    return false;
+}
+constexpr int kLdsDummy = 3 * 32 + 4;  // dummy message slots after the E real ones (DV=3)
 
 namespace ldpc {
 

@@ -272,63 +272,66 @@ struct BpArgs {
     int32_t *trial;  // [B][max_iters+1]
     // generic kernel, messages in global scratch
     float *scratch;
+    // LDS kernel lane layout (ldpc_graph::lane_var / lane_slot)
+    const int32_t *lane_var, *lane_slot;
 };
 
 // ---------------------------------------------------------------------------
 // 2a. Regular fast path: whole codeword resident in LDS.
-//   LDS  msg[E] fp32 (check-major slots: check c = [c*DC, c*DC+DC)),
-//        hs[E] u8 hard decision per slot (ET / MC only), curve (MC only).
-//   Thread t owns checks t, t+T, ... and variables t + i*T (i < VPT); its
-//   variables' slot indices and channel LLRs stay in VGPRs for the whole
-//   decode.  Iteration = check phase (contiguous float2 LDS traffic, tanh /
-//   min-sum in registers) | barrier | variable phase (DV random LDS gathers,
-//   posterior, extrinsic write-back) | barrier.
+//   LDS  msg[E + dummies] fp32 (check-major slots: check c = [c*DC, c*DC+DC)),
+//        hs[...] u8 hard decision per slot (ET only), curve (MC only).
+//   Thread t owns checks t, t+T, ... and the variables of lane positions
+//   p = t + i*T (i < VPT) of the host-built conflict-aware layout: every 32
+//   consecutive positions (one half-wave LDS access) hit 32 distinct banks as far
+//   as the graph allows; padding positions address private dummy slots.
+//   Slot indices (packed 2 x 16 bit) and channel LLRs stay in VGPRs for the
+//   whole decode.  Iteration = check phase (contiguous float2 LDS traffic, tanh /
+//   min-sum in registers) | barrier | variable phase (DV gathers, posterior,
+//   extrinsic write-back) | barrier.  Channel LLRs in and posteriors out are
+//   staged through LDS so their HBM traffic stays coalesced.
 // ---------------------------------------------------------------------------
 template <int DV, int DC, int T, int VPT, int ALGO, bool ET, bool MC>
 __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     float *msg = reinterpret_cast<float *>(smem);
-    // DV dummy slots after the E real ones absorb the gathers of the padded
-    // variables v >= n (L = 0, messages stay 0), so the variable phase needs no
-    // per-variable guard.
-    const int Ep = a.E + 4;
+    const int Ep = a.E + kLdsDummy;
     uint8_t *hs = smem + (size_t)Ep * 4;
     int *curve = reinterpret_cast<int *>(smem + (((size_t)Ep * 5 + 15) & ~(size_t)15));
     const int tid = threadIdx.x;
-    const int n = a.n, m = a.m, iters = a.max_iters;
-    constexpr int NS = VPT * DV;            // slots owned through my variables
-    constexpr bool KEEP_POST = ET && !MC;   // posterior must survive the loop
+    const int n = a.n, m = a.m, E = a.E, iters = a.max_iters;
+    constexpr int NS = VPT * DV;  // slots reached through my variables
 
     for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
         const uint64_t cw = a.first_cw + (uint64_t)b;
-        // slot indices packed two per VGPR (E < 65536 on this path)
-        uint32_t sp[(NS + 1) / 2];
-        float L[VPT];
-        float pr[KEEP_POST ? VPT : 1];
-        int err0 = 0;
-#pragma unroll
-        for (int q = 0; q < (NS + 1) / 2; ++q) sp[q] = 0;
-#pragma unroll
-        for (int i = 0; i < VPT; ++i) {
-            const int v = tid + i * T;
-            L[i] = 0.0f;
-            if (v < n) {
-                L[i] = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
-                err0 += (L[i] < 0.0f);
-            }
-#pragma unroll
-            for (int j = 0; j < DV; ++j) {
-                const int q = i * DV + j;
-                const int slot = v < n ? a.vslot[v * DV + j] : a.E + j;
-                sp[q >> 1] |= (uint32_t)slot << (16 * (q & 1));
-            }
-            if constexpr (KEEP_POST) pr[i] = L[i];
-        }
-#define SLOT(i, j) ((int)((sp[((i) * DV + (j)) >> 1] >> (16 * (((i) * DV + (j)) & 1))) & 0xFFFFu))
+        // ---- stage the channel LLRs (coalesced) ----
         __syncthreads();  // previous codeword fully drained (msg, curve)
         if (MC) {
             for (int i = tid; i <= iters; i += T) curve[i] = 0;
         }
+        int err0 = 0;
+        for (int v = tid; v < n; v += T) {
+            const float l = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
+            msg[v] = l;
+            err0 += (l < 0.0f);
+        }
+        __syncthreads();
+        uint32_t sp[(NS + 1) / 2];
+        float L[VPT];
+#pragma unroll
+        for (int q = 0; q < (NS + 1) / 2; ++q) sp[q] = 0;
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            const int p = tid + i * T;
+            const int vv = a.lane_var[p];
+            L[i] = vv >= 0 ? msg[vv] : 0.0f;
+#pragma unroll
+            for (int j = 0; j < DV; ++j) {
+                const int q = i * DV + j;
+                sp[q >> 1] |= (uint32_t)a.lane_slot[p * DV + j] << (16 * (q & 1));
+            }
+        }
+#define SLOT(i, j) ((int)((sp[((i) * DV + (j)) >> 1] >> (16 * (((i) * DV + (j)) & 1))) & 0xFFFFu))
+        __syncthreads();  // staging read before the message initialisation overwrites it
 #pragma unroll
         for (int i = 0; i < VPT; ++i) {
 #pragma unroll
@@ -339,56 +342,45 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             const int w = wave_sum(err0);
             if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[0], w);
         }
-        if (!ET && !MC && iters == 0) {
-#pragma unroll
-            for (int i = 0; i < VPT; ++i) {
-                const int v = tid + i * T;
-                if (v < n) {
-                    if (a.post) a.post[(size_t)b * n + v] = L[i];
-                    if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(L[i] < 0.0f);
-                }
-            }
-        }
 
-        // the last fixed-count iteration writes the outputs instead of
-        // extrinsic messages; two straight-line copies keep the gathers free
-        // of per-variable branches.
+        // variable phase; FINAL (the last fixed-count iteration) keeps the
+        // posteriors in registers instead of writing extrinsic messages.
+        float pr[MC ? 1 : VPT];
+        if constexpr (!MC) {
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) pr[i] = L[i];
+        }
         auto var_phase = [&](auto final_tag) {
             constexpr bool FINAL = decltype(final_tag)::value;
             int errs = 0;
 #pragma unroll
             for (int i = 0; i < VPT; ++i) {
-                const int v = tid + i * T;
-                {
-                    float cv[DV];
-                    float s = L[i];
+                float cv[DV];
+                float s = L[i];
 #pragma unroll
-                    for (int j = 0; j < DV; ++j) {
-                        cv[j] = msg[SLOT(i, j)];
-                        s += cv[j];
-                    }
-                    if constexpr (FINAL) {
-                        if (v < n) {
-                            if (a.post) a.post[(size_t)b * n + v] = s;
-                            if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
-                        }
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = s - cv[j];
-                    }
-                    if constexpr (KEEP_POST) pr[i] = s;
-                    if constexpr (ET) {
-#pragma unroll
-                        for (int j = 0; j < DV; ++j) hs[SLOT(i, j)] = (uint8_t)(s < 0.0f);
-                    }
-                    if constexpr (MC) errs += (v < n) & (s < 0.0f);
+                for (int j = 0; j < DV; ++j) {
+                    cv[j] = msg[SLOT(i, j)];
+                    s += cv[j];
                 }
+                if constexpr (!FINAL) {
+#pragma unroll
+                    for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = s - cv[j];
+                }
+                if constexpr (!MC) {
+                    if (FINAL || ET) pr[i] = s;
+                }
+                if constexpr (ET) {
+#pragma unroll
+                    for (int j = 0; j < DV; ++j) hs[SLOT(i, j)] = (uint8_t)(s < 0.0f);
+                }
+                if constexpr (MC) errs += (SLOT(i, 0) < E) & (s < 0.0f);
                 // at most two variables' gathers in flight per thread (VGPR
-                // budget of 4 waves/SIMD; the 16 waves of the CU hide LDS latency)
+                // budget of 4 waves/SIMD; the CU's 16 waves hide LDS latency)
                 if (i & 1) __builtin_amdgcn_sched_barrier(0);
             }
             return errs;
         };
+
         int it = 0;
         for (; it < iters; ++it) {
             if (ET && it > 0) {  // syndrome of the previous iteration's hard decision
@@ -429,13 +421,11 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                 }
             }
             __syncthreads();
-            // variable phase.  Launder the packed slots so the compiler cannot
-            // hoist their unpacking out of the iteration loop (that would pin
-            // VPT*DV unpacked addresses in VGPRs and spill).
+            // Launder the packed slots so the compiler cannot hoist their
+            // unpacking out of the iteration loop (VPT*DV pinned addresses spill).
 #pragma unroll
             for (int q = 0; q < (NS + 1) / 2; ++q) asm volatile("" : "+v"(sp[q]));
-            // fixed-count decode: the last variable phase runs after the loop and
-            // writes the outputs (keeps its 64-bit output addresses out of the loop)
+            // fixed-count decode: the last variable phase runs after the loop
             if (!ET && !MC && it == iters - 1) break;
             const int errs = var_phase(std::false_type{});
             if (MC) {
@@ -444,28 +434,29 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             }
         }
         if (!ET && !MC && iters > 0) {
-#pragma unroll
-            for (int q = 0; q < (NS + 1) / 2; ++q) asm volatile("" : "+v"(sp[q]));
             (void)var_phase(std::true_type{});
             it = iters;
         }
 #undef SLOT
-        if (MC) {
+        if constexpr (MC) {
             __syncthreads();
             int32_t *tr = a.trial + (size_t)b * (iters + 1);
             const int last = curve[it];
             for (int i = tid; i <= iters; i += T) tr[i] = i <= it ? curve[i] : last;
             if (tid == 0) a.its[b] = it;
         } else {
-            if constexpr (KEEP_POST) {
+            // posteriors out through LDS (coalesced HBM writes)
+            __syncthreads();
 #pragma unroll
-                for (int i = 0; i < VPT; ++i) {
-                    const int v = tid + i * T;
-                    if (v < n) {
-                        if (a.post) a.post[(size_t)b * n + v] = pr[i];
-                        if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(pr[i] < 0.0f);
-                    }
-                }
+            for (int i = 0; i < VPT; ++i) {
+                const int vv = a.lane_var[tid + i * T];
+                if (vv >= 0) msg[vv] = pr[i];
+            }
+            __syncthreads();
+            for (int v = tid; v < n; v += T) {
+                const float s = msg[v];
+                if (a.post) a.post[(size_t)b * n + v] = s;
+                if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
             }
             if (a.its && tid == 0) a.its[b] = it;
         }
@@ -772,7 +763,7 @@ BecArgs bec_args(const ldpc_graph &g) {
 enum class BpPath { Lds36, Generic8, Generic16, Generic32, GenericG8, GenericG16, GenericG32, None };
 
 size_t lds36_bytes(const ldpc_graph &g, int iters, bool et, bool mc) {
-    const size_t Ep = (size_t)g.E + 4;
+    const size_t Ep = (size_t)g.E + kLdsDummy;
     size_t s = Ep * 4;
     if (et || mc) s = (Ep * 5 + 15) & ~(size_t)15;
     if (mc) s += (size_t)(iters + 1) * 4;
@@ -785,7 +776,7 @@ size_t generic_lds_bytes(const ldpc_graph &g, int iters, bool mc) {
 
 BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc) {
     if (!g.consistent) return BpPath::None;
-    if (g.dv == 3 && g.dc == 6 && g.n <= 13 * 1024 && lds36_bytes(g, iters, et, mc) <= kLdsMax - 2048)
+    if (g.lane_var && g.dv == 3 && g.dc == 6 && lds36_bytes(g, iters, et, mc) <= kLdsMax - 2048)
         return BpPath::Lds36;
     const int d = g.max_cdeg;
     if (d > 32) return BpPath::None;
@@ -807,14 +798,15 @@ hipError_t launch_lds36_vpt(const ldpc_graph &g, BpArgs a, size_t lds, hipStream
 template <int ALGO, bool ET, bool MC>
 hipError_t launch_lds36(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     const size_t lds = lds36_bytes(g, a.max_iters, ET, MC);
-    if (g.n <= 256) return launch_lds36_vpt<1, 256, ALGO, ET, MC>(g, a, lds, s);
-    if (g.n <= 512) return launch_lds36_vpt<2, 256, ALGO, ET, MC>(g, a, lds, s);
-    if (g.n <= 1024) return launch_lds36_vpt<4, 256, ALGO, ET, MC>(g, a, lds, s);
-    if (g.n <= 2048) return launch_lds36_vpt<8, 256, ALGO, ET, MC>(g, a, lds, s);
-    if (g.n <= 4 * 1024) return launch_lds36_vpt<4, 1024, ALGO, ET, MC>(g, a, lds, s);
-    if (g.n <= 8 * 1024) return launch_lds36_vpt<8, 1024, ALGO, ET, MC>(g, a, lds, s);
-    if (g.n <= 10 * 1024) return launch_lds36_vpt<10, 1024, ALGO, ET, MC>(g, a, lds, s);
-    return launch_lds36_vpt<13, 1024, ALGO, ET, MC>(g, a, lds, s);
+    a.lane_var = g.lane_var;
+    a.lane_slot = g.lane_slot;
+#define LDS36_CASE(TT, VV) \
+    if (g.lane_T == TT && g.lane_VPT == VV) return launch_lds36_vpt<VV, TT, ALGO, ET, MC>(g, a, lds, s);
+    LDS36_CASE(256, 1) LDS36_CASE(256, 2) LDS36_CASE(256, 3) LDS36_CASE(256, 5) LDS36_CASE(256, 9)
+    LDS36_CASE(1024, 2) LDS36_CASE(1024, 3) LDS36_CASE(1024, 5) LDS36_CASE(1024, 6) LDS36_CASE(1024, 9)
+    LDS36_CASE(1024, 11) LDS36_CASE(1024, 14)
+#undef LDS36_CASE
+    return hipErrorInvalidValue;
 }
 
 template <int MAXDC, int ALGO, bool ET, bool MC, bool GMEM>

@@ -149,6 +149,21 @@ int ldpc_mc_batch_dev(const ldpc_graph *g, int channel, float param, uint64_t se
                       int64_t stop_frame_errors, int64_t *d_counters, void *stream);
 
 /* ---------------------------------------------------------------------- */
+/* Diagnostics (host only, no GPU needed)                                  */
+/* ---------------------------------------------------------------------- */
+/*
+ * The conflict-aware lane layout the LDS-resident soft kernel uses for this
+ * graph: *T threads x *VPT variables per thread; lane_var int32[T*VPT]
+ * (-1 = padding), lane_slot int32[T*VPT*dv].  Pass NULL arrays to query T/VPT.
+ */
+int ldpc_debug_lane_layout(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list,
+                           int n, int k, int dv, int dc, int32_t *T, int32_t *VPT, int32_t *lane_var,
+                           int32_t *lane_slot);
+
+/* Name of the soft kernel a graph dispatches to (tests / bench). */
+const char *ldpc_bp_kernel_name(const ldpc_graph *g, int early_stop);
+
+/* ---------------------------------------------------------------------- */
 /* Misc                                                                    */
 /* ---------------------------------------------------------------------- */
 const char *ldpc_last_error(void);

@@ -129,3 +129,37 @@ def test_csv_writer_format(tmp_path, monkeypatch):
     ps.write_message_passing_file("x.csv", [0.4, 0.3], 0.1, 0.02)
     txt = open(tmp_path / "report_data" / "simulation_data" / "x.csv").read().splitlines()
     assert txt == ["0.4", "0.3", "Message passing block-wise error,0.1", "Message passing bit-wise error,0.02"]
+
+
+def _layout(g):
+    from iib_project_ldpc_codes_amd import _native
+    L = _native.lib()
+    T, V = ct.c_int32(), ct.c_int32()
+    rc = L.ldpc_debug_lane_layout(g.variable_lookup.ctypes.data, g.check_lookup.ctypes.data, g.n, g.k, g.dv, g.dc,
+                                  ct.byref(T), ct.byref(V), None, None)
+    assert rc == 0
+    lv = np.zeros(T.value * V.value, np.int32)
+    ls = np.zeros(T.value * V.value * g.dv, np.int32)
+    rc = L.ldpc_debug_lane_layout(g.variable_lookup.ctypes.data, g.check_lookup.ctypes.data, g.n, g.k, g.dv, g.dc,
+                                  ct.byref(T), ct.byref(V), lv.ctypes.data, ls.ctypes.data)
+    assert rc == 0
+    return T.value, V.value, lv, ls.reshape(-1, g.dv)
+
+
+@pytest.mark.parametrize("n", [1000, 10000])
+def test_lane_layout_is_conflict_aware_permutation(n):
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = TannerGraph.random_regular(n, 3, 6, seed=4)
+    T, V, lv, ls = _layout(g)
+    assert T * V >= n and T % 64 == 0
+    real = lv >= 0
+    assert np.array_equal(np.sort(lv[real]), np.arange(n))  # every variable exactly once
+    vslot = g.to_csr()[3].reshape(n, 3)
+    np.testing.assert_array_equal(ls[real], vslot[lv[real]])
+    E = g.num_edges
+    assert np.all(ls[~real] >= E)  # padding lanes use private dummy slots
+    # cost model: LDS cycles per half-wave access = busiest-bank multiplicity
+    mult = [np.bincount(ls[q:q + 32, j] % 32, minlength=32).max() for q in range(0, ls.shape[0], 32) for j in range(3)]
+    assert np.mean(mult) < 1.25, np.mean(mult)
+    base = [np.bincount(vslot[q:q + 32, j] % 32, minlength=32).max() for q in range(0, n - 31, 32) for j in range(3)]
+    assert np.mean(base) > 2.5  # the naive order would conflict
