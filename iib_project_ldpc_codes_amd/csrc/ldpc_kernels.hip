@@ -208,28 +208,38 @@ __global__ __launch_bounds__(T) void bec_kernel(BecArgs a) {
 // ===========================================================================
 // 2. Soft flooding BP (no reference counterpart; oracle_bp_decode defines it)
 // ===========================================================================
-// Raw CDNA transcendentals (v_exp_f32 = 2^x, v_log_f32 = log2, v_rcp_f32; ~1 ulp):
-// ~7 VALU per conversion instead of the IEEE division / range-reduced libm paths.
-__device__ __forceinline__ float tanh_half(float x) {
-    const float e = __builtin_amdgcn_exp2f(fabsf(x) * -1.44269504088896341f);  // exp(-|x|)
-    const float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
-    return copysignf(t, x);
+// Sum-product runs in the log2 domain: messages are LLR / ln 2, so
+// exp(-|x|) is one v_exp_f32 (2^x) with a -|.| source modifier and the check
+// output log((1+p)/(1-p)) is one v_log_f32 (log2); channel LLRs are scaled by
+// log2(e) on the way in and posteriors by ln 2 on the way out.  Raw CDNA
+// transcendentals (v_exp_f32, v_log_f32, v_rcp_f32; ~1 ulp); 2/(1+e) - 1 and
+// 2/(1-|p|) - 1 by fma: 11 VALU (4 transcendental) per edge.
+template <int ALGO> struct Domain {
+    static constexpr float in = ALGO == 0 ? 1.44269504088896341f : 1.0f;   // LLR -> message units
+    static constexpr float out = ALGO == 0 ? 0.693147180559945309f : 1.0f; // message units -> LLR
+};
+
+__device__ __forceinline__ float tanh_half_l2(float x2) {  // tanh(x/2), x = x2 ln 2
+    const float e = __builtin_amdgcn_exp2f(-fabsf(x2));
+    const float t = __builtin_fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + e), -1.0f);
+    return copysignf(t, x2);
 }
 
-__device__ __forceinline__ float atanh2(float p) {
-    p = __builtin_amdgcn_fmed3f(p, -kPMax, kPMax);
-    const float r = (1.0f + p) * __builtin_amdgcn_rcpf(1.0f - p);
-    return __builtin_amdgcn_logf(r) * 0.693147180559945309f;
+__device__ __forceinline__ float atanh2_l2(float p) {  // 2 atanh(p) / ln 2
+    const float a = fminf(fabsf(p), kPMax);
+    const float q = __builtin_fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f - a), -1.0f);
+    return copysignf(__builtin_amdgcn_logf(q), p);
 }
 
 // Check-node update over D messages in registers (padding: +inf, neutral for
-// both rules).  Same operation order as oracle check_update_{spa,ms}.
+// both rules).  Same product / min order as oracle check_update_{spa,ms};
+// min-sum is bit-exact with it, sum-product agrees to the stated tolerance.
 template <int ALGO, int D>
 __device__ __forceinline__ void check_update(float (&x)[D], float alpha) {
     if (ALGO == 0) {
         float t[D];
 #pragma unroll
-        for (int i = 0; i < D; ++i) t[i] = tanh_half(x[i]);
+        for (int i = 0; i < D; ++i) t[i] = tanh_half_l2(x[i]);
         float pre[D], suf[D];
         pre[0] = 1.0f;
 #pragma unroll
@@ -238,7 +248,7 @@ __device__ __forceinline__ void check_update(float (&x)[D], float alpha) {
 #pragma unroll
         for (int i = D - 2; i >= 0; --i) suf[i] = suf[i + 1] * t[i + 1];
 #pragma unroll
-        for (int i = 0; i < D; ++i) x[i] = atanh2(pre[i] * suf[i]);
+        for (int i = 0; i < D; ++i) x[i] = atanh2_l2(pre[i] * suf[i]);
     } else {
         float m1 = __builtin_inff(), m2 = __builtin_inff();
         int i1 = 0, neg = 0;
@@ -311,7 +321,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
         int err0 = 0;
         for (int v = tid; v < n; v += T) {
             const float l = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
-            msg[v] = l;
+            msg[v] = l * Domain<ALGO>::in;
             err0 += (l < 0.0f);
         }
         __syncthreads();
@@ -455,7 +465,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             __syncthreads();
             for (int v = tid; v < n; v += T) {
                 const float s = msg[v];
-                if (a.post) a.post[(size_t)b * n + v] = s;
+                if (a.post) a.post[(size_t)b * n + v] = s * Domain<ALGO>::out;
                 if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
             }
             if (a.its && tid == 0) a.its[b] = it;
@@ -493,9 +503,10 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
         int err0 = 0;
         for (int v = tid; v < n; v += T) {
             const float l = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
-            Ls[v] = l;
+            const float l2 = l * Domain<ALGO>::in;
+            Ls[v] = l2;
             err0 += (l < 0.0f);
-            for (int e = a.vptr[v]; e < a.vptr[v + 1]; ++e) msg[a.vslot[e]] = l;
+            for (int e = a.vptr[v]; e < a.vptr[v + 1]; ++e) msg[a.vslot[e]] = l2;
             if (!MC) {
                 if (a.post) a.post[(size_t)b * n + v] = l;
                 if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(l < 0.0f);
@@ -542,7 +553,7 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
                 }
                 errs += (s < 0.0f);
                 if (!MC) {
-                    if (a.post) a.post[(size_t)b * n + v] = s;
+                    if (a.post) a.post[(size_t)b * n + v] = s * Domain<ALGO>::out;
                     if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
                 }
             }

@@ -10,7 +10,8 @@ cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 BENCH="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 $BENCH > $OUT/trace_bench.log 2>&1 || exit $?
 echo "trace ok"; tail -1 $OUT/trace_bench.log
-PMCB="bench.py --steps 1 --warmup 0 --batch ${PMC_BATCH:-16384} --no-cpu-baseline --no-extras"
+PMC_BATCH=${PMC_BATCH:-65536}
+PMCB="bench.py --steps 1 --warmup 0 --batch $PMC_BATCH --no-cpu-baseline --no-extras"
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
@@ -25,4 +26,5 @@ WRITE_SIZE
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS
 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT}
 GROUPS
+python3 scripts/pmc_summary.py $OUT $PMC_BATCH > $OUT/pmc_summary.txt 2>&1; cat $OUT/pmc_summary.txt
 exit 0
