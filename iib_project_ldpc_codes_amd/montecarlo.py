@@ -6,8 +6,8 @@ curve; a second launch applies the expurgation filter
 rule (parallel_simulator.py:198) and accumulates int64 counters on the device.
 
 Multi-GPU (one process per GPU, torch.distributed): trials shard by index --
-rank r of W runs batches (round * W + r); the only collective is one
-all-reduce of the counter vector per round (RCCL over xGMI with backend
+rank r of W runs the batch of trials [(round*W + r)*B, +B); the only collective
+is one all-reduce of the counter vector per round (RCCL over xGMI with backend
 "nccl", gloo on CPU), used for the global stop rule and the final result.
 """
 import time
@@ -18,9 +18,25 @@ from . import _native
 from .decoder import ALGOS, CHANNELS
 
 
+def device_executor(mc):
+    """Batch executor backed by ldpc_mc_batch_dev on the current HIP device."""
+    torch = mc.torch
+
+    def run(first_cw, B, stop_frame_errors, counters, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream()
+        rc = _native.lib().ldpc_mc_batch_dev(mc.graph.handle(), mc.channel, mc.param, mc.seed, int(first_cw),
+                                             int(B), mc.max_iters, mc.algo, mc.alpha, int(mc.early_stop),
+                                             mc.expurgation, int(stop_frame_errors), counters.data_ptr(),
+                                             s.cuda_stream)
+        _native.check(rc, "ldpc_mc_batch_dev")
+    return run
+
+
 class MonteCarlo:
+    """counters = [trials, frame_errors, bit_errors, iterations, curve[0..max_iters]] (int64)."""
+
     def __init__(self, graph, channel, param, max_iters, algo="spa", alpha=1.0, early_stop=True,
-                 expurgation=-1, seed=0, batch=4096, process_group=None):
+                 expurgation=-1, seed=0, batch=4096, process_group=None, executor=None, device=None):
         import torch
         self.torch = torch
         self.graph = graph
@@ -38,37 +54,34 @@ class MonteCarlo:
         self.dist = dist if (dist.is_available() and dist.is_initialized()) else None
         self.rank = self.dist.get_rank(process_group) if self.dist else 0
         self.world = self.dist.get_world_size(process_group) if self.dist else 1
-        self.device = torch.device("cuda", torch.cuda.current_device())
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if executor is None else torch.device("cpu")
+        self.device = torch.device(device)
         self.counters = torch.zeros(_native.MC_NCOUNT + self.max_iters + 1, dtype=torch.int64, device=self.device)
+        self.executor = executor if executor is not None else device_executor(self)
         self.rounds = 0
 
     def run_batch(self, first_cw, B, stop_frame_errors=0, stream=None):
-        s = stream if stream is not None else self.torch.cuda.current_stream()
-        rc = _native.lib().ldpc_mc_batch_dev(self.graph.handle(), self.channel, self.param, self.seed,
-                                             int(first_cw), int(B), self.max_iters, self.algo, self.alpha,
-                                             int(self.early_stop), self.expurgation, int(stop_frame_errors),
-                                             self.counters.data_ptr(), s.cuda_stream)
-        _native.check(rc, "ldpc_mc_batch_dev")
+        if stream is None:
+            self.executor(first_cw, B, stop_frame_errors, self.counters)
+        else:
+            self.executor(first_cw, B, stop_frame_errors, self.counters, stream)
 
     def _global(self):
         c = self.counters.clone()
         if self.dist is not None and self.world > 1:
-            backend = self.dist.get_backend(self.pg)
-            if backend == "gloo":
+            if self.dist.get_backend(self.pg) == "gloo":
                 c = c.cpu()
-                self.dist.all_reduce(c, group=self.pg)
-            else:
-                self.dist.all_reduce(c, group=self.pg)
+            self.dist.all_reduce(c, group=self.pg)
         return c.cpu().numpy()
 
     def run(self, num_tests, stop_frame_errors=200, time_limit=None):
-        """Run until stop_frame_errors frame errors (global), num_tests trials or time_limit seconds."""
+        """Run rounds until the global counters reach stop_frame_errors frame errors or
+        num_tests trials, or time_limit seconds pass (parallel_simulator.py:198)."""
         t0 = time.time()
-        first_round = self.rounds
         while True:
-            r = self.rounds
-            first_cw = (r * self.world + self.rank) * self.batch
-            # single process: exact sequential stop inside the batch
+            first_cw = (self.rounds * self.world + self.rank) * self.batch
+            # one process: the exact sequential stop happens inside the batch
             stop = stop_frame_errors if self.world == 1 else 0
             self.run_batch(first_cw, self.batch, stop)
             self.rounds += 1
@@ -78,8 +91,6 @@ class MonteCarlo:
             if num_tests and g[0] >= num_tests:
                 break
             if time_limit is not None and time.time() - t0 > time_limit:
-                break
-            if self.rounds - first_round > 10 ** 9:
                 break
         return self.results(g)
 

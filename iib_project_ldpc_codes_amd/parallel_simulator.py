@@ -113,38 +113,31 @@ def _filename(prefix, parameter_set, n, k, dv, dc, iterations, num, code_number=
 
 
 def _device_loop(graph_fn, parameter_set, expurgation, stop_frames, time_limit):
-    """Fused device trial loop; graph_fn(i) gives the graph for batch i (fixed or fresh)."""
+    """Fused device trial loop; graph_fn(i) gives the graph for batch i (fixed code:
+    always the same; ensemble: a fresh draw per ``trials_per_code`` trials)."""
     from .montecarlo import MonteCarlo
-    import torch
     num_tests = parameter_set["num_tests"]
     iterations = parameter_set["iterations"]
     batch = int(parameter_set.get("batch", DEFAULT_BATCH))
     seed = int(parameter_set.get("seed", parameter_set.get("filenumber", 0)))
-    per_code = int(parameter_set.get("trials_per_code", 0))  # 0: fixed code
-    counters = None
-    done = 0
+    per_code = int(parameter_set.get("trials_per_code", 0))  # 0: one fixed code
     t0 = datetime.now()
-    i = 0
-    while True:
+    counters, res, done, i = None, None, 0, 0
+    while done < num_tests:
         B = min(batch if per_code == 0 else per_code, num_tests - done)
-        if B <= 0:
-            break
-        g = graph_fn(i)
-        mc = MonteCarlo(g, "bec", parameter_set["BEC"], iterations, expurgation=expurgation, seed=seed)
+        mc = MonteCarlo(graph_fn(i), "bec", parameter_set["BEC"], iterations, expurgation=expurgation,
+                        seed=seed, batch=B)
         if counters is not None:
             mc.counters.copy_(counters)
-        mc.run_batch(done, B, stop_frames)
+        mc.run_batch(done, B, stop_frames)  # trial indices continue across batches
         counters = mc.counters
         res = mc.results()
         done = res["num_tests"]
         i += 1
-        if res["frame_errors"] >= stop_frames or done >= num_tests:
+        if res["frame_errors"] >= stop_frames:
             break
         if time_limit and (datetime.now() - t0).total_seconds() >= time_limit:
             break
-        if res["num_tests"] < sum([0]):  # pragma: no cover
-            break
-    torch.cuda.synchronize()
     return res
 
 

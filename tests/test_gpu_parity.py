@@ -302,3 +302,29 @@ def test_mc_minsum_bsc_exact(torch):
     want[2] = int(h.sum())
     want[3] = int(final_its.sum())
     np.testing.assert_array_equal(got, want)
+
+
+def test_parallel_simulator_fixed_code_device_engine(torch, tmp_path, monkeypatch):
+    """run_simulation_fixed_ldpc (parallel_simulator.py:274-401 surface) on the device engine ==
+    the oracle's sequential loop over the same Philox trials, including the 200-frame stop."""
+    from iib_project_ldpc_codes_amd import parallel_simulator as ps
+    monkeypatch.setattr(ps, "base_directory", str(tmp_path) + "/")
+    params = dict(BEC=0.42, num_tests=3000, iterations=30, n=500, dv=3, dc=6, filenumber=1, optimal=False,
+                  message_passing=True, batch=256)
+    res = ps.run_simulation_fixed_ldpc(params)
+    g = ps.load_or_create_fixed_code(1, 500, 3, 6)
+    want = _oracle_bec_counters(g, 0.42, 1, 3000, 30, stop=200)
+    assert res["num_tests"] == want[0] and res["frame_errors"] == want[1] == 200
+    assert res["bit_errors"] == want[2]
+    np.testing.assert_allclose(res["error_curve"], want[4:] / (500 * want[0]))
+    rows = open(tmp_path / "report_data" / "simulation_data" / res["filename"]).read().splitlines()
+    assert len(rows) == 30 + 1 + 2 and rows[-2].startswith("Message passing block-wise error")
+
+
+def test_parallel_simulator_per_trial_engine(torch, tmp_path, monkeypatch):
+    """The reference's own loop (numpy channel, one drop-in call per trial) runs end to end."""
+    from iib_project_ldpc_codes_amd import parallel_simulator as ps
+    monkeypatch.setattr(ps, "base_directory", str(tmp_path) + "/")
+    res = ps.run_simulation_fixed_ldpc(dict(BEC=0.3, num_tests=50, iterations=20, n=200, dv=3, dc=6, filenumber=2,
+                                            optimal=False, message_passing=True, engine="per_trial"))
+    assert res["num_tests"] == 50 and res["error_curve"][0] == pytest.approx(0.3, abs=0.05)
