@@ -16,8 +16,19 @@
 namespace ldpc {
 namespace {
 
-constexpr float kPMax = 0.99999994f;  // 1 - 2^-24, as oracle/ldpc_oracle.c
 constexpr int kWave = 64;
+#ifndef LDPC_VAR_GROUP
+#define LDPC_VAR_GROUP 2  // variables per sched_barrier group in the LDS kernel's variable phase
+#endif
+#ifndef LDPC_ABLATE_CHECK
+#define LDPC_ABLATE_CHECK 0
+#endif
+#ifndef LDPC_ABLATE_VARW
+#define LDPC_ABLATE_VARW 0
+#endif
+#ifndef LDPC_CHECK_UNROLL
+#define LDPC_CHECK_UNROLL 1
+#endif
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (the rocRAND philox4x32_10 stream: rocrand_init(seed,
@@ -208,47 +219,51 @@ __global__ __launch_bounds__(T) void bec_kernel(BecArgs a) {
 // ===========================================================================
 // 2. Soft flooding BP (no reference counterpart; oracle_bp_decode defines it)
 // ===========================================================================
-// Sum-product runs in the log2 domain: messages are LLR / ln 2, so
-// exp(-|x|) is one v_exp_f32 (2^x) with a -|.| source modifier and the check
-// output log((1+p)/(1-p)) is one v_log_f32 (log2); channel LLRs are scaled by
-// log2(e) on the way in and posteriors by ln 2 on the way out.  Raw CDNA
-// transcendentals (v_exp_f32, v_log_f32, v_rcp_f32; ~1 ulp); 2/(1+e) - 1 and
-// 2/(1-|p|) - 1 by fma: 11 VALU (4 transcendental) per edge.
+// Sum-product runs in the log2 domain (messages are LLR / ln 2) and in the
+// ratio form of oracle check_update_spa: e_i = 2^-min(|x_i|, 23) is one
+// v_exp_f32, the exclusive product of tanh(x_i/2) = a_i / b_i (a_i = sign*(1-e_i),
+// b_i = 1+e_i) is N_j / D_j from prefix/suffix products, and 2 atanh(N/D) / ln 2 =
+// log2((D+N) / (D-N)) is one v_rcp_f32 + one v_log_f32 -- three transcendentals
+// per edge.  Channel LLRs are scaled by log2(e) in, posteriors by ln 2 out.
 template <int ALGO> struct Domain {
     static constexpr float in = ALGO == 0 ? 1.44269504088896341f : 1.0f;   // LLR -> message units
     static constexpr float out = ALGO == 0 ? 0.693147180559945309f : 1.0f; // message units -> LLR
 };
 
-__device__ __forceinline__ float tanh_half_l2(float x2) {  // tanh(x/2), x = x2 ln 2
-    const float e = __builtin_amdgcn_exp2f(-fabsf(x2));
-    const float t = __builtin_fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + e), -1.0f);
-    return copysignf(t, x2);
-}
-
-__device__ __forceinline__ float atanh2_l2(float p) {  // 2 atanh(p) / ln 2
-    const float a = fminf(fabsf(p), kPMax);
-    const float q = __builtin_fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f - a), -1.0f);
-    return copysignf(__builtin_amdgcn_logf(q), p);
-}
-
-// Check-node update over D messages in registers (padding: +inf, neutral for
-// both rules).  Same product / min order as oracle check_update_{spa,ms};
-// min-sum is bit-exact with it, sum-product agrees to the stated tolerance.
+// Check-node update over D messages in registers; entries i >= d are padding
+// (+inf for min-sum, unit factors for sum-product).  Same product / min order as
+// oracle check_update_{spa,ms}: min-sum is bit-exact with it, sum-product agrees
+// to the stated tolerance.
 template <int ALGO, int D>
-__device__ __forceinline__ void check_update(float (&x)[D], float alpha) {
+__device__ __forceinline__ void check_update(float (&x)[D], float alpha, int d = D) {
     if (ALGO == 0) {
-        float t[D];
+        float na[D], db[D];
 #pragma unroll
-        for (int i = 0; i < D; ++i) t[i] = tanh_half_l2(x[i]);
-        float pre[D], suf[D];
-        pre[0] = 1.0f;
+        for (int i = 0; i < D; ++i) {
+            const float e = __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x[i]), 0.0f, 23.0f));
+            na[i] = i < d ? copysignf(1.0f - e, x[i]) : 1.0f;
+            db[i] = i < d ? 1.0f + e : 1.0f;
+        }
+        float pa[D], sa[D], pb[D], sb[D];
+        pa[0] = 1.0f;
+        pb[0] = 1.0f;
 #pragma unroll
-        for (int i = 1; i < D; ++i) pre[i] = pre[i - 1] * t[i - 1];
-        suf[D - 1] = 1.0f;
+        for (int i = 1; i < D; ++i) {
+            pa[i] = pa[i - 1] * na[i - 1];
+            pb[i] = pb[i - 1] * db[i - 1];
+        }
+        sa[D - 1] = 1.0f;
+        sb[D - 1] = 1.0f;
 #pragma unroll
-        for (int i = D - 2; i >= 0; --i) suf[i] = suf[i + 1] * t[i + 1];
+        for (int i = D - 2; i >= 0; --i) {
+            sa[i] = sa[i + 1] * na[i + 1];
+            sb[i] = sb[i + 1] * db[i + 1];
+        }
 #pragma unroll
-        for (int i = 0; i < D; ++i) x[i] = atanh2_l2(pre[i] * suf[i]);
+        for (int i = 0; i < D; ++i) {
+            const float N = pa[i] * sa[i], Dn = pb[i] * sb[i];
+            x[i] = __builtin_amdgcn_logf((Dn + N) * __builtin_amdgcn_rcpf(Dn - N));
+        }
     } else {
         float m1 = __builtin_inff(), m2 = __builtin_inff();
         int i1 = 0, neg = 0;
@@ -373,8 +388,13 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     s += cv[j];
                 }
                 if constexpr (!FINAL) {
+#if LDPC_ABLATE_VARW
+#pragma unroll
+                    for (int j = 0; j < DV; ++j) { float y = s - cv[j]; asm volatile("" :: "v"(y)); }
+#else
 #pragma unroll
                     for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = s - cv[j];
+#endif
                 }
                 if constexpr (!MC) {
                     if (FINAL || ET) pr[i] = s;
@@ -386,7 +406,8 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                 if constexpr (MC) errs += (SLOT(i, 0) < E) & (s < 0.0f);
                 // at most two variables' gathers in flight per thread (VGPR
                 // budget of 4 waves/SIMD; the CU's 16 waves hide LDS latency)
-                if (i & 1) __builtin_amdgcn_sched_barrier(0);
+                if (LDPC_VAR_GROUP > 0 && (i % LDPC_VAR_GROUP) == LDPC_VAR_GROUP - 1)
+                    __builtin_amdgcn_sched_barrier(0);
             }
             return errs;
         };
@@ -406,6 +427,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                 __syncthreads();
             }
             // check phase
+#pragma unroll LDPC_CHECK_UNROLL
             for (int c = tid; c < m; c += T) {
                 float x[DC];
                 if constexpr (DC % 2 == 0) {
@@ -420,7 +442,12 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 #pragma unroll
                     for (int s = 0; s < DC; ++s) x[s] = msg[c * DC + s];
                 }
+#if LDPC_ABLATE_CHECK
+#pragma unroll
+                for (int s = 0; s < DC; ++s) x[s] = x[s] * 0.5f;  // timing ablation only
+#else
                 check_update<ALGO, DC>(x, a.alpha);
+#endif
                 if constexpr (DC % 2 == 0) {
                     float2 *p = reinterpret_cast<float2 *>(msg + c * DC);
 #pragma unroll
@@ -535,7 +562,7 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
                 float x[MAXDC];
 #pragma unroll
                 for (int s = 0; s < MAXDC; ++s) x[s] = s < d ? msg[s0 + s] : __builtin_inff();
-                check_update<ALGO, MAXDC>(x, a.alpha);
+                check_update<ALGO, MAXDC>(x, a.alpha, d);
 #pragma unroll
                 for (int s = 0; s < MAXDC; ++s)
                     if (s < d) msg[s0 + s] = x[s];
