@@ -237,32 +237,27 @@ template <int ALGO> struct Domain {
 template <int ALGO, int D>
 __device__ __forceinline__ void check_update(float (&x)[D], float alpha, int d = D) {
     if (ALGO == 0) {
-        float na[D], db[D];
+        // (a_i, b_i) pairs live in float2 so 1 -+ e and both product chains are
+        // v_pk_add_f32 / v_pk_mul_f32 (two lanes of work per VALU issue).
+        float2 ab[D];
 #pragma unroll
         for (int i = 0; i < D; ++i) {
             const float e = __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x[i]), 0.0f, 23.0f));
-            na[i] = i < d ? copysignf(1.0f - e, x[i]) : 1.0f;
-            db[i] = i < d ? 1.0f + e : 1.0f;
+            float2 t = make_float2(1.0f, 1.0f) + make_float2(-e, e);
+            t.x = copysignf(t.x, x[i]);
+            ab[i] = i < d ? t : make_float2(1.0f, 1.0f);
         }
-        float pa[D], sa[D], pb[D], sb[D];
-        pa[0] = 1.0f;
-        pb[0] = 1.0f;
+        float2 pre[D], suf[D];
+        pre[0] = make_float2(1.0f, 1.0f);
 #pragma unroll
-        for (int i = 1; i < D; ++i) {
-            pa[i] = pa[i - 1] * na[i - 1];
-            pb[i] = pb[i - 1] * db[i - 1];
-        }
-        sa[D - 1] = 1.0f;
-        sb[D - 1] = 1.0f;
+        for (int i = 1; i < D; ++i) pre[i] = pre[i - 1] * ab[i - 1];
+        suf[D - 1] = make_float2(1.0f, 1.0f);
 #pragma unroll
-        for (int i = D - 2; i >= 0; --i) {
-            sa[i] = sa[i + 1] * na[i + 1];
-            sb[i] = sb[i + 1] * db[i + 1];
-        }
+        for (int i = D - 2; i >= 0; --i) suf[i] = suf[i + 1] * ab[i + 1];
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            const float N = pa[i] * sa[i], Dn = pb[i] * sb[i];
-            x[i] = __builtin_amdgcn_logf((Dn + N) * __builtin_amdgcn_rcpf(Dn - N));
+            const float2 nd = pre[i] * suf[i];  // (N_i, D_i)
+            x[i] = __builtin_amdgcn_logf((nd.y + nd.x) * __builtin_amdgcn_rcpf(nd.y - nd.x));
         }
     } else {
         float m1 = __builtin_inff(), m2 = __builtin_inff();
