@@ -84,9 +84,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % max(ndev, 1))
+    backend = os.environ.get("LDPC_DIST_BACKEND", "nccl")  # gloo: rehearse N ranks on one GPU
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local % max(ndev, 1)))
+        else:
+            dist.init_process_group(backend)
 
     from iib_project_ldpc_codes_amd import decoder
     from iib_project_ldpc_codes_amd.graph import TannerGraph
@@ -124,7 +129,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
 
@@ -153,6 +158,22 @@ def main():
         b.record(stream)
         torch.cuda.synchronize()
         extras["minsum_50it_codewords_per_s"] = B / (a.elapsed_time(b) * 1e-3)
+        # BEC erasure decoding (message_passing.c semantics, bit-exact): configs[0] and configs[4] shapes
+        for key, n_b, eps, its_b, Bb in (("bec_cfg1_n1000_eps0.4_50it", 1000, 0.40, 50, 65536),
+                                         ("bec_cfg5_n64800_eps0.4_200it", 64800, 0.40, 200, 4096)):
+            gb = TannerGraph.random_regular(n_b, DV, DC, seed=1)
+            w0 = decoder.channel_dev("bec", eps, 5, 0, n_b, Bb)
+            w = w0.clone()
+            decoder.bec_decode_dev(gb, w, its_b)
+            w = w0.clone()
+            torch.cuda.synchronize()
+            a.record(stream)
+            _, _, its_bec = decoder.bec_decode_dev(gb, w, its_b)
+            b.record(stream)
+            torch.cuda.synchronize()
+            extras[key] = {"codewords_per_s": Bb / (a.elapsed_time(b) * 1e-3),
+                           "mean_iterations": float(its_bec.float().mean().item()), "batch": Bb}
+            del w, w0
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1:
