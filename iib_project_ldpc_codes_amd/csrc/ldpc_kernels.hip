@@ -234,7 +234,17 @@ template <int ALGO> struct Domain {
 // (+inf for min-sum, unit factors for sum-product).  Same product / min order as
 // oracle check_update_{spa,ms}: min-sum is bit-exact with it, sum-product agrees
 // to the stated tolerance.
-template <int ALGO, int D>
+// v->c message "on the wire" of the LDS kernel: sum-product sends
+// w = sign(x) * 2^-min(|x|, 23) (the check rule's e_i with the sign of x), so the
+// exponential is evaluated in the LDS-bound variable phase instead of the
+// VALU-bound check phase; min-sum sends x itself.
+template <int ALGO>
+__device__ __forceinline__ float v2c_wire(float x) {
+    if (ALGO == 0) return copysignf(__builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x), 0.0f, 23.0f)), x);
+    return x;
+}
+
+template <int ALGO, int D, bool WIRE = false>
 __device__ __forceinline__ void check_update(float (&x)[D], float alpha, int d = D) {
     if (ALGO == 0) {
         // (a_i, b_i) pairs live in float2 so 1 -+ e and both product chains are
@@ -242,7 +252,8 @@ __device__ __forceinline__ void check_update(float (&x)[D], float alpha, int d =
         float2 ab[D];
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            const float e = __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x[i]), 0.0f, 23.0f));
+            const float e = WIRE ? fabsf(x[i])
+                                 : __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x[i]), 0.0f, 23.0f));
             float2 t = make_float2(1.0f, 1.0f) + make_float2(-e, e);
             t.x = copysignf(t.x, x[i]);
             ab[i] = i < d ? t : make_float2(1.0f, 1.0f);
@@ -354,8 +365,9 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
         __syncthreads();  // staging read before the message initialisation overwrites it
 #pragma unroll
         for (int i = 0; i < VPT; ++i) {
+            const float w = v2c_wire<ALGO>(L[i]);
 #pragma unroll
-            for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = L[i];
+            for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = w;
         }
         __syncthreads();
         if (MC) {
@@ -388,7 +400,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     for (int j = 0; j < DV; ++j) { float y = s - cv[j]; asm volatile("" :: "v"(y)); }
 #else
 #pragma unroll
-                    for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = s - cv[j];
+                    for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = v2c_wire<ALGO>(s - cv[j]);
 #endif
                 }
                 if constexpr (!MC) {
@@ -441,7 +453,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 #pragma unroll
                 for (int s = 0; s < DC; ++s) x[s] = x[s] * 0.5f;  // timing ablation only
 #else
-                check_update<ALGO, DC>(x, a.alpha);
+                check_update<ALGO, DC, true>(x, a.alpha);
 #endif
                 if constexpr (DC % 2 == 0) {
                     float2 *p = reinterpret_cast<float2 *>(msg + c * DC);
