@@ -39,7 +39,7 @@ struct DevBuf {
 };
 
 struct Workspace {
-    DevBuf trial, its, cutoff, scratch, words, llr, post, hard, errors, itsb;
+    DevBuf trial, its, cutoff, scratch, words, llr, post, hard, errors, itsb, gchk, gvar, gatt;
 };
 std::map<std::pair<int, void *>, Workspace> g_ws;  // (device, stream)
 
@@ -629,6 +629,79 @@ int ldpc_mc_batch_dev(const ldpc_graph *g, int channel, float param, uint64_t se
     int32_t *trial = static_cast<int32_t *>(ws.trial.p), *its = static_cast<int32_t *>(ws.its.p);
     LDPC_HIP(launch_mc_decode(*g, channel, p, p2, seed, first_cw, B, max_iters, algo, alpha, early_stop, trial, its,
                               s, scratch));
+    LDPC_HIP(launch_mc_reduce(trial, its, B, max_iters, expurgation, stop_frame_errors, d_counters,
+                              static_cast<int32_t *>(ws.cutoff.p), s));
+    return LDPC_OK;
+}
+
+// --------------------------- random graphs / ensemble MC -------------------
+static int check_regular_shape(int n, int dv, int dc) {
+    LDPC_REQUIRE(n > 0 && dv > 0 && dc > 1 && (long)n * dv % dc == 0 && (long)n * dv < (1L << 30),
+                 "need n*dv divisible by dc (regular configuration model)");
+    return LDPC_OK;
+}
+
+int ldpc_sample_regular_dev(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
+                            int32_t *d_check_lookup, int32_t *d_variable_lookup, int32_t *d_attempts, void *stream) {
+    int rc = check_regular_shape(n, dv, dc);
+    if (rc) return rc;
+    LDPC_REQUIRE(d_check_lookup && d_variable_lookup && G >= 0, "bad sampler arguments");
+    rc = require_device();
+    if (rc) return rc;
+    LDPC_HIP(launch_sample_regular(n, dv, dc, seed, first_graph, G, d_check_lookup, d_variable_lookup, d_attempts,
+                                   1 << 20, static_cast<hipStream_t>(stream)));
+    return LDPC_OK;
+}
+
+int ldpc_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G, int32_t *check_lookup,
+                        int32_t *variable_lookup, int32_t *attempts) {
+    int rc = check_regular_shape(n, dv, dc);
+    if (rc) return rc;
+    LDPC_REQUIRE(check_lookup && variable_lookup && G >= 0, "bad sampler arguments");
+    rc = require_device();
+    if (rc) return rc;
+    const size_t E = (size_t)n * dv;
+    std::lock_guard<std::mutex> lk(g_mu);
+    Workspace &ws = workspace(nullptr);
+    LDPC_HIP(ws.gchk.ensure(E * G * 4));
+    LDPC_HIP(ws.gvar.ensure(E * G * 4));
+    LDPC_HIP(ws.gatt.ensure((size_t)G * 4 + 4));
+    LDPC_HIP(launch_sample_regular(n, dv, dc, seed, first_graph, G, static_cast<int32_t *>(ws.gchk.p),
+                                   static_cast<int32_t *>(ws.gvar.p), static_cast<int32_t *>(ws.gatt.p), 1 << 20,
+                                   nullptr));
+    LDPC_HIP(hipDeviceSynchronize());
+    LDPC_HIP(hipMemcpy(check_lookup, ws.gchk.p, E * G * 4, hipMemcpyDeviceToHost));
+    LDPC_HIP(hipMemcpy(variable_lookup, ws.gvar.p, E * G * 4, hipMemcpyDeviceToHost));
+    if (attempts) LDPC_HIP(hipMemcpy(attempts, ws.gatt.p, (size_t)G * 4, hipMemcpyDeviceToHost));
+    return LDPC_OK;
+}
+
+int ldpc_mc_ensemble_batch_dev(int n, int dv, int dc, int channel, float param, uint64_t seed, uint64_t first_cw,
+                               int B, int max_iters, int expurgation, int64_t stop_frame_errors, int64_t *d_counters,
+                               void *stream) {
+    int rc = check_regular_shape(n, dv, dc);
+    if (rc) return rc;
+    LDPC_REQUIRE(channel == LDPC_CH_BEC, "ensemble Monte-Carlo is BEC-only (as parallel_simulator.py:168-272)");
+    LDPC_REQUIRE(d_counters && B >= 0 && max_iters >= 0, "bad MC arguments");
+    float p, p2;
+    rc = channel_params(channel, param, &p, &p2);
+    if (rc) return rc;
+    rc = require_device();
+    if (rc) return rc;
+    if (B == 0) return LDPC_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t E = (size_t)n * dv;
+    std::lock_guard<std::mutex> lk(g_mu);
+    Workspace &ws = workspace(stream);
+    LDPC_HIP(ws.gchk.ensure(E * B * 4));
+    LDPC_HIP(ws.gvar.ensure(E * B * 4));
+    LDPC_HIP(ws.trial.ensure(sizeof(int32_t) * (size_t)B * (max_iters + 1)));
+    LDPC_HIP(ws.its.ensure(sizeof(int32_t) * (size_t)B));
+    LDPC_HIP(ws.cutoff.ensure(16));
+    int32_t *chk = static_cast<int32_t *>(ws.gchk.p), *var = static_cast<int32_t *>(ws.gvar.p);
+    int32_t *trial = static_cast<int32_t *>(ws.trial.p), *its = static_cast<int32_t *>(ws.its.p);
+    LDPC_HIP(launch_sample_regular(n, dv, dc, seed, first_cw, B, chk, var, nullptr, 1 << 20, s));
+    LDPC_HIP(launch_mc_bec_ensemble(n, dv, dc, chk, var, p, seed, first_cw, B, max_iters, trial, its, s));
     LDPC_HIP(launch_mc_reduce(trial, its, B, max_iters, expurgation, stop_frame_errors, d_counters,
                               static_cast<int32_t *>(ws.cutoff.p), s));
     return LDPC_OK;

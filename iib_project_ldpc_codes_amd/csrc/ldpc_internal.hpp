@@ -79,6 +79,17 @@ hipError_t launch_mc_reduce(const int32_t *trial, const int32_t *trial_its, int 
                             int expurgation, int64_t stop_frame_errors, int64_t *d_counters,
                             int32_t *d_cutoff, hipStream_t stream);
 
+// Random regular graphs on the device (law of random_code_generator.c), one
+// thread per graph; attempts[g] = number of permutations drawn (negative if
+// max_attempts was hit without a valid graph).
+hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
+                                 int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts,
+                                 int max_attempts, hipStream_t stream);
+// BEC Monte-Carlo where trial b decodes on graph b of (check_lookup, variable_lookup).
+hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,
+                                  float p, uint64_t seed, uint64_t first_cw, int B, int max_iters, int32_t *trial,
+                                  int32_t *trial_its, hipStream_t stream);
+
 // Kernel-choice introspection for tests / bench ("lds36", "generic", ...).
 const char *bp_kernel_name(const ldpc_graph &g, int early_stop);
 

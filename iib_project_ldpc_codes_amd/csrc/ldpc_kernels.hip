@@ -124,6 +124,8 @@ struct BecArgs {
     ChanArgs ch;
     uint64_t first_cw;
     int32_t *trial;  // [B][max_iters+1]
+    // ensemble mode: codeword b decodes on its own graph (cvar / vchk + b*graph_stride)
+    int64_t graph_stride;
 };
 
 template <int T, bool MC>
@@ -136,6 +138,8 @@ __global__ __launch_bounds__(T) void bec_kernel(BecArgs a) {
     int32_t *errs = reinterpret_cast<int32_t *>(smem);
     uint8_t *mvc = smem + ((iters * 4 + 15) & ~15);
     uint8_t *cs = mvc + ((n + 15) & ~15);
+    const int32_t *cvar = a.cvar + (size_t)b * a.graph_stride;
+    const int32_t *vchk = a.vchk + (size_t)b * a.graph_stride;
 
     int init_cnt = 0;
     if (MC) {
@@ -169,7 +173,7 @@ __global__ __launch_bounds__(T) void bec_kernel(BecArgs a) {
             const int s1 = a.dc > 0 ? s0 + a.dc : a.cptr[c + 1];
             int ne = 0, par = 0;
             for (int s = s0; s < s1; ++s) {
-                const int x = mvc[a.cvar[s]];
+                const int x = mvc[cvar[s]];
                 ne += (x == 2);
                 par ^= (x & 1);
             }
@@ -184,7 +188,7 @@ __global__ __launch_bounds__(T) void bec_kernel(BecArgs a) {
                 const int e0 = a.dv > 0 ? v * a.dv : a.vptr[v];
                 const int e1 = a.dv > 0 ? e0 + a.dv : a.vptr[v + 1];
                 for (int e = e0; e < e1; ++e) {
-                    const int c = a.vchk[e];
+                    const int c = vchk[e];
                     if (c >= 0) {
                         const int y = cs[c];
                         if (y != 2) x = y;
@@ -607,6 +611,99 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
 }
 
 // ===========================================================================
+// 2c. Random regular (dv, dc) graphs: the law of random_code_generator.c:21-67
+//
+// Configuration model: a uniform permutation of the n*dv sockets, check c =
+// positions [c*dc, c*dc+dc), variable of a socket = socket / dv, and a whole-
+// graph redraw whenever a check holds a variable twice (:39-47).  One thread per
+// graph runs Fisher-Yates from the end, so check c is complete as soon as
+// position c*dc is fixed and a bad check aborts the attempt at once -- the same
+// conditional law as drawing the whole permutation and rejecting it (the next
+// attempt reshuffles the current array, as the reference's recursion does).
+// Draw k of graph g is word k%4 of Philox(ctr = {k/4, 'GRPH', g_lo, g_hi},
+// key = seed); j = uniform on [0, i] by Lemire's multiply with rejection
+// (the reference's rand() % (i+1) carries a small modulo bias we do not copy).
+// Output: check_lookup[g][E] (variable ids, check-major) and variable_lookup
+// [g][E] (each variable's checks ascending), the reference's edge-list format.
+// oracle_sample_regular restates this bit for bit.
+// ===========================================================================
+constexpr uint32_t kGraphTag = 0x48505247u;  // 'GRPH'
+
+struct GraphRng {
+    uint32_t k0, k1, g0, g1;
+    uint64_t k = 0;
+    uint4 blk;
+    __device__ __forceinline__ uint32_t next() {
+        const uint32_t w = (uint32_t)(k & 3);
+        if (w == 0) blk = philox_block((uint32_t)(k >> 2), kGraphTag, g0, g1, k0, k1);
+        ++k;
+        return pick4(blk, w);
+    }
+    __device__ __forceinline__ uint32_t below(uint32_t range) {  // uniform on [0, range)
+        uint64_t m = (uint64_t)next() * range;
+        uint32_t l = (uint32_t)m;
+        if (l < range) {
+            const uint32_t t = (0u - range) % range;
+            while (l < t) {
+                m = (uint64_t)next() * range;
+                l = (uint32_t)m;
+            }
+        }
+        return (uint32_t)(m >> 32);
+    }
+};
+
+__global__ __launch_bounds__(64) void sample_regular_kernel(int n, int dv, int dc, uint32_t k0, uint32_t k1,
+                                                            uint64_t first_graph, int G, int32_t *check_lookup,
+                                                            int32_t *variable_lookup, int32_t *attempts,
+                                                            int max_attempts) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    const int E = n * dv;
+    int32_t *seq = check_lookup + (size_t)g * E;
+    int32_t *vl = variable_lookup + (size_t)g * E;
+    const uint64_t gid = first_graph + (uint64_t)g;
+    GraphRng rng{k0, k1, (uint32_t)gid, (uint32_t)(gid >> 32)};
+    for (int s = 0; s < E; ++s) seq[s] = s;
+    int att = 0;
+    bool ok = false;
+    while (!ok && att < max_attempts) {
+        ++att;
+        ok = true;
+        for (int i = E - 1; i >= 1; --i) {
+            const int j = (int)rng.below((uint32_t)i + 1u);
+            const int t = seq[i];
+            seq[i] = seq[j];
+            seq[j] = t;
+            if (i % dc == 0) {  // check i/dc complete
+                for (int x = i; x < i + dc && ok; ++x)
+                    for (int y = x + 1; y < i + dc; ++y)
+                        if (seq[x] / dv == seq[y] / dv) { ok = false; break; }
+                if (!ok) break;
+            }
+        }
+        if (ok) {  // check 0 completes with the last swap
+            for (int x = 0; x < dc && ok; ++x)
+                for (int y = x + 1; y < dc; ++y)
+                    if (seq[x] / dv == seq[y] / dv) { ok = false; break; }
+        }
+    }
+    if (attempts) attempts[g] = ok ? att : -att;
+    // variable_lookup: socket v*dv+t -> its check, then each variable's checks ascending
+    for (int s = 0; s < E; ++s) vl[seq[s]] = s / dc;
+    for (int v = 0; v < n; ++v) {
+        int32_t *r = vl + (size_t)v * dv;
+        for (int x = 1; x < dv; ++x) {  // insertion sort (dv is tiny)
+            const int key = r[x];
+            int y = x - 1;
+            while (y >= 0 && r[y] > key) { r[y + 1] = r[y]; --y; }
+            r[y + 1] = key;
+        }
+    }
+    for (int s = 0; s < E; ++s) seq[s] = seq[s] / dv;  // check_lookup = variable ids
+}
+
+// ===========================================================================
 // 3. Stand-alone channel (rocRAND philox4x32_10 device API)
 // ===========================================================================
 __global__ __launch_bounds__(256) void channel_kernel(int kind, float p, float p2, uint64_t seed,
@@ -980,6 +1077,36 @@ hipError_t launch_mc_decode(const ldpc_graph &g, int channel, float p, float p2,
     a.its = trial_its;
     a.scratch = d_scratch;
     return dispatch_bp_algo<true>(g, a, algo, early_stop, stream);
+}
+
+hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
+                                 int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts,
+                                 int max_attempts, hipStream_t stream) {
+    if (G <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sample_regular_kernel, dim3((G + 63) / 64), dim3(64), 0, stream, n, dv, dc, (uint32_t)seed,
+                       (uint32_t)(seed >> 32), first_graph, G, check_lookup, variable_lookup, attempts, max_attempts);
+    return hipGetLastError();
+}
+
+hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,
+                                  float p, uint64_t seed, uint64_t first_cw, int B, int max_iters, int32_t *trial,
+                                  int32_t *trial_its, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    ldpc_graph g{};
+    g.n = n;
+    g.m = n * dv / dc;
+    g.dv = dv;
+    g.dc = dc;
+    BecArgs a = bec_args(g);
+    a.cvar = check_lookup;
+    a.vchk = variable_lookup;
+    a.graph_stride = (int64_t)n * dv;
+    a.max_iters = max_iters;
+    a.ch = make_chan(0, p, 0.0f, seed);
+    a.first_cw = first_cw;
+    a.trial = trial;
+    a.its = trial_its;
+    return run_bec<true>(g, a, B, stream);
 }
 
 hipError_t launch_mc_reduce(const int32_t *trial, const int32_t *trial_its, int B, int max_iters,

@@ -73,6 +73,21 @@ class TannerGraph:
             return cls(var, chk, n, k, dv, dc)
         raise RuntimeError("random_regular: too many redraws")
 
+    @classmethod
+    def sample_device(cls, n, dv, dc, seed=0, graph_id=0):
+        """Graph `graph_id` of the on-device sampler (ldpc_sample_regular; same law as
+        random_code_generator.c, counter-based so any graph can be regenerated)."""
+        k = int(n * (dc - dv) / dc)
+        chk = np.zeros(n * dv, np.int32)
+        var = np.zeros(n * dv, np.int32)
+        att = np.zeros(1, np.int32)
+        rc = _native.lib().ldpc_sample_regular(n, dv, dc, int(seed), int(graph_id), 1, chk.ctypes.data,
+                                               var.ctypes.data, att.ctypes.data)
+        _native.check(rc, "ldpc_sample_regular")
+        if att[0] <= 0:
+            raise RuntimeError("sampler hit its attempt cap")
+        return cls(var, chk, n, k, dv, dc)
+
     # ---------------------------------------------------------------- helpers
     @property
     def num_edges(self):

@@ -32,6 +32,28 @@ def device_executor(mc):
     return run
 
 
+def ensemble_executor(mc, n, dv, dc):
+    """Batch executor for ensemble mode: trial t decodes on its own random (dv, dc)
+    graph t (ldpc_mc_ensemble_batch_dev; parallel_simulator.py:198-231 draws a fresh
+    code per trial)."""
+    torch = mc.torch
+
+    def run(first_cw, B, stop_frame_errors, counters, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream()
+        rc = _native.lib().ldpc_mc_ensemble_batch_dev(n, dv, dc, mc.channel, mc.param, mc.seed, int(first_cw), int(B),
+                                                      mc.max_iters, mc.expurgation, int(stop_frame_errors),
+                                                      counters.data_ptr(), s.cuda_stream)
+        _native.check(rc, "ldpc_mc_ensemble_batch_dev")
+    return run
+
+
+class _Ensemble:
+    """Stand-in for a graph in ensemble mode (only n is needed by the counters)."""
+
+    def __init__(self, n, dv, dc):
+        self.n, self.dv, self.dc = n, dv, dc
+
+
 class MonteCarlo:
     """counters = [trials, frame_errors, bit_errors, iterations, curve[0..max_iters]] (int64)."""
 
@@ -58,8 +80,16 @@ class MonteCarlo:
             device = torch.device("cuda", torch.cuda.current_device()) if executor is None else torch.device("cpu")
         self.device = torch.device(device)
         self.counters = torch.zeros(_native.MC_NCOUNT + self.max_iters + 1, dtype=torch.int64, device=self.device)
-        self.executor = executor if executor is not None else device_executor(self)
+        if executor is None:
+            executor = (ensemble_executor(self, graph.n, graph.dv, graph.dc) if isinstance(graph, _Ensemble)
+                        else device_executor(self))
+        self.executor = executor
         self.rounds = 0
+
+    @classmethod
+    def ensemble(cls, n, dv, dc, channel, param, max_iters, **kw):
+        """Fresh random (dv, dc) code per trial (BEC; parallel_simulator.run_simulation)."""
+        return cls(_Ensemble(n, dv, dc), channel, param, max_iters, **kw)
 
     def run_batch(self, first_cw, B, stop_frame_errors=0, stream=None):
         if stream is None:

@@ -141,6 +141,30 @@ def _device_loop(graph_fn, parameter_set, expurgation, stop_frames, time_limit):
     return res
 
 
+def _device_ensemble_loop(parameter_set, expurgation, stop_frames, time_limit):
+    """Ensemble mode on the device: trial t draws its own code (ldpc_sample_regular law)
+    and channel word, decoded and counted in fused batches."""
+    from .montecarlo import MonteCarlo
+    n, dv, dc = parameter_set["n"], parameter_set["dv"], parameter_set["dc"]
+    mc = MonteCarlo.ensemble(n, dv, dc, "bec", parameter_set["BEC"], parameter_set["iterations"],
+                             expurgation=expurgation, seed=int(parameter_set.get("seed", 0)),
+                             batch=int(parameter_set.get("batch", 1024)))
+    t0 = datetime.now()
+    num_tests = parameter_set["num_tests"]
+    while True:
+        done = int(mc.counters[0].item())
+        B = min(mc.batch, num_tests - done)
+        if B <= 0:
+            break
+        mc.run_batch(done, B, stop_frames)
+        res = mc.results()
+        if res["frame_errors"] >= stop_frames or res["num_tests"] >= num_tests:
+            break
+        if time_limit and (datetime.now() - t0).total_seconds() >= time_limit:
+            break
+    return mc.results()
+
+
 def _per_trial_loop(LDPC_fn, parameter_set, expurgation, stop_frames, time_limit):
     """The reference's own loop (parallel_simulator.py:198-244) with per-trial drop-in calls."""
     sim_BEC = BEC(parameter_set["BEC"])
@@ -178,11 +202,10 @@ def _run(parameter_set, fixed, expurgation=-1, prefix="regular_code", time_limit
         fn_graph = lambda i: code  # noqa: E731
     else:
         fn_graph = lambda i: TannerGraph.random_regular(n, dv, dc, seed=(seed, i))  # noqa: E731
-    if engine == "device":
-        ps = dict(parameter_set)
-        if not fixed:
-            ps.setdefault("trials_per_code", 1)
-        res = _device_loop(fn_graph, ps, expurgation, 200, time_limit)
+    if engine == "device" and not fixed:
+        res = _device_ensemble_loop(parameter_set, expurgation, 200, time_limit)
+    elif engine == "device":
+        res = _device_loop(fn_graph, parameter_set, expurgation, 200, time_limit)
     else:
         def ldpc_fn(i):
             g = fn_graph(i)

@@ -149,6 +149,37 @@ int ldpc_mc_batch_dev(const ldpc_graph *g, int channel, float param, uint64_t se
                       int64_t stop_frame_errors, int64_t *d_counters, void *stream);
 
 /* ---------------------------------------------------------------------- */
+/* Random regular graphs + ensemble Monte-Carlo           */
+/* ---------------------------------------------------------------------- */
+/*
+ * Replaces generate_random_code (random_code_generator.c:21-67, called per
+ * trial at parallel_simulator.py:215 / parallel_simulator_expurgated.py:221-223):
+ * G graphs first_graph .. first_graph+G-1 of the (dv, dc) configuration model
+ * with whole-graph redraw while any check holds a variable twice, in the
+ * reference's edge-list format: check_lookup int32[G][n*dv] (variables of check
+ * c at [c*dc, c*dc+dc)), variable_lookup int32[G][n*dv] (checks of each variable,
+ * ascending).  Counter-based (Philox, key = seed): graph g is the same whatever
+ * G / first_graph batch it is drawn in.  attempts int32[G] (may be NULL): number
+ * of permutations drawn for each graph.  The dense parity-check matrix is never
+ * built.
+ */
+int ldpc_sample_regular_dev(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
+                            int32_t *d_check_lookup, int32_t *d_variable_lookup, int32_t *d_attempts,
+                            void *stream);
+int ldpc_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
+                        int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts);
+
+/*
+ * Ensemble BEC Monte-Carlo batch (run_simulation, parallel_simulator.py:168-272;
+ * expurgated :169-285): trial t = first_cw + b draws graph t and channel word t,
+ * decodes with message_passing semantics and accumulates counters exactly as
+ * ldpc_mc_batch_dev (expurgation, sequential stop rule).
+ */
+int ldpc_mc_ensemble_batch_dev(int n, int dv, int dc, int channel, float param, uint64_t seed,
+                               uint64_t first_cw, int B, int max_iters, int expurgation,
+                               int64_t stop_frame_errors, int64_t *d_counters, void *stream);
+
+/* ---------------------------------------------------------------------- */
 /* Diagnostics (host only, no GPU needed)                                  */
 /* ---------------------------------------------------------------------- */
 /*

@@ -44,6 +44,8 @@ def lib():
         _lib.oracle_channel.restype = None
         _lib.oracle_density_evolution.argtypes = [ct.c_double, i, i, i, ct.c_double, P]
         _lib.oracle_density_evolution.restype = i
+        _lib.oracle_sample_regular.argtypes = [i, i, i, u64, u64, i, P, P]
+        _lib.oracle_sample_regular.restype = i
         _lib.oracle_num_threads.argtypes = []
         _lib.oracle_num_threads.restype = i
     return _lib
@@ -133,6 +135,15 @@ def channel(kind, p, seed, first_cw, n, B):
     out = np.zeros((B, n), np.int8 if kind == CH_BEC else np.float32)
     lib().oracle_channel(kind, p, p2, seed, first_cw, n, B, _p(out))
     return out
+
+
+def sample_regular(n, dv, dc, seed, graph, max_attempts=1 << 20):
+    """Restatement of the device sampler (law of random_code_generator.c).
+    Returns (check_lookup, variable_lookup, attempts)."""
+    chk = np.zeros(n * dv, np.int32)
+    var = np.zeros(n * dv, np.int32)
+    att = lib().oracle_sample_regular(n, dv, dc, seed, graph, max_attempts, _p(chk), _p(var))
+    return chk, var, att
 
 
 def density_evolution(eps, iterations, dv, dc, threshold=0.0):

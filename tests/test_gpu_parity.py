@@ -328,3 +328,53 @@ def test_parallel_simulator_per_trial_engine(torch, tmp_path, monkeypatch):
     res = ps.run_simulation_fixed_ldpc(dict(BEC=0.3, num_tests=50, iterations=20, n=200, dv=3, dc=6, filenumber=2,
                                             optimal=False, message_passing=True, engine="per_trial"))
     assert res["num_tests"] == 50 and res["error_curve"][0] == pytest.approx(0.3, abs=0.05)
+
+
+# ------------------------------------------------------------ random graphs
+@pytest.mark.parametrize("n,dv,dc", [(1000, 3, 6), (90, 2, 3), (96, 4, 8), (10000, 3, 6)])
+def test_device_sampler_matches_oracle(torch, n, dv, dc):
+    from iib_project_ldpc_codes_amd import _native
+    L = _native.lib()
+    G, E = 6, n * dv
+    chk = np.zeros(G * E, np.int32)
+    var = np.zeros(G * E, np.int32)
+    att = np.zeros(G, np.int32)
+    rc = L.ldpc_sample_regular(n, dv, dc, 31, 1000, G, chk.ctypes.data, var.ctypes.data, att.ctypes.data)
+    assert rc == 0
+    for g in range(G):
+        ochk, ovar, oatt = oracle.sample_regular(n, dv, dc, 31, 1000 + g)
+        assert att[g] == oatt > 0
+        np.testing.assert_array_equal(chk[g * E:(g + 1) * E], ochk)
+        np.testing.assert_array_equal(var[g * E:(g + 1) * E], ovar)
+
+
+def test_ensemble_mc_matches_oracle(torch):
+    """ldpc_mc_ensemble_batch_dev: trial t = graph t + channel word t, counters exact."""
+    from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
+    n, B, iters, eps, seed = 200, 96, 20, 0.40, 17
+    mc = MonteCarlo.ensemble(n, 3, 6, "bec", eps, iters, seed=seed, batch=B)
+    mc.run_batch(0, B)
+    torch.cuda.synchronize()
+    got = mc.counters.cpu().numpy()
+    want = np.zeros(4 + iters + 1, np.int64)
+    words = oracle.channel(oracle.CH_BEC, eps, seed, 0, n, B)
+    for b in range(B):
+        chk, var, _ = oracle.sample_regular(n, 3, 6, seed, b)
+        _, err, it = oracle.message_passing(words[b], iters, var, chk, n, n // 2, 3, 6)
+        curve = np.insert(err, 0, int(np.count_nonzero(words[b] == 2)))
+        want[4:] += curve
+        want[1] += curve[-1] != 0
+        want[2] += curve[-1]
+        want[0] += 1
+        want[3] += it
+    np.testing.assert_array_equal(got, want)
+
+
+def test_parallel_simulator_ensemble_device(torch, tmp_path, monkeypatch):
+    from iib_project_ldpc_codes_amd import parallel_simulator_expurgated as pse
+    from iib_project_ldpc_codes_amd import parallel_simulator as ps
+    monkeypatch.setattr(ps, "base_directory", str(tmp_path) + "/")
+    res = pse.run_simulation(dict(BEC=0.45, num_tests=2000, iterations=40, n=600, dv=3, dc=6, seed=3, optimal=False,
+                                  message_passing=True, expurgation=2, batch=512))
+    assert 0 < res["num_tests"] <= 2000 and res["frame_errors"] <= 200
+    assert res["filename"].startswith("regular_code_expurgated=2_BEC=0.45")

@@ -163,3 +163,38 @@ def test_lane_layout_is_conflict_aware_permutation(n):
     assert np.mean(mult) < 1.25, np.mean(mult)
     base = [np.bincount(vslot[q:q + 32, j] % 32, minlength=32).max() for q in range(0, n - 31, 32) for j in range(3)]
     assert np.mean(base) > 2.5  # the naive order would conflict
+
+
+def test_oracle_sampler_law_matches_reference_generator():
+    """The device sampler's restatement (oracle_sample_regular) draws from the law of
+    random_code_generator.c: valid graphs, consistent lists, same 4-cycle statistic."""
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built")
+
+    def c4(chk, n, m):
+        H = np.zeros((m, n), np.int64)
+        for c in range(m):
+            H[c, chk[c * 6:(c + 1) * 6]] = 1
+        O = H @ H.T
+        np.fill_diagonal(O, 0)
+        return int((O * (O - 1) // 2).sum() // 2)
+
+    ref = [c4(oracle.ref_generate_random_code(40, 3, 6)[0], 40, 20) for _ in range(300)]
+    ours = []
+    for gid in range(300):
+        chk, var, att = oracle.sample_regular(40, 3, 6, 11, gid)
+        assert att > 0
+        rows = chk.reshape(20, 6)
+        assert all(len(set(r)) == 6 for r in rows)
+        v = var.reshape(40, 3)
+        assert np.all(np.diff(v, axis=1) > 0)
+        for x in range(40):
+            assert set(np.nonzero(rows == x)[0]) == set(v[x])
+        ours.append(c4(chk, 40, 20))
+    assert abs(np.mean(ref) - np.mean(ours)) < 4 * np.sqrt((np.var(ref) + np.var(ours)) / 300)
+
+
+def test_oracle_sampler_attempts_geometric():
+    """Whole-graph redraw: attempts ~ Geometric(P(valid)), P(valid) ~ exp(-5) for (3,6)."""
+    a = np.array([oracle.sample_regular(1000, 3, 6, 7, g)[2] for g in range(200)])
+    assert np.all(a > 0) and 90 < a.mean() < 250
