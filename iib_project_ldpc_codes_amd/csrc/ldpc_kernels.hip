@@ -8,6 +8,7 @@
 //   parallel_simulator.py:198-244  -> mc_* (per-trial statistics + stop rule)
 #include <rocrand/rocrand_kernel.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "ldpc_internal.hpp"
@@ -653,6 +654,42 @@ struct GraphRng {
     }
 };
 
+// Both kernels permute variable ids (socket / dv) rather than sockets: the
+// draws are identical and every output depends on the socket only through its
+// variable, so the graphs are the same -- without integer divisions on the
+// dependent swap chain.  Position bookkeeping uses countdowns, not modulo.
+template <typename Idx, typename Acc>
+__device__ __forceinline__ bool sample_one(int E, int dc, GraphRng &rng, Acc S, int max_attempts, int &att) {
+    bool ok = false;
+    att = 0;
+    auto check_ok = [&](int first) {
+        for (int x = first; x < first + dc; ++x) {
+            const Idx vx = S(x);
+            for (int y = x + 1; y < first + dc; ++y)
+                if (S(y) == vx) return false;
+        }
+        return true;
+    };
+    while (!ok && att < max_attempts) {
+        ++att;
+        ok = true;
+        int to_check = (E - 1) % dc;  // steps until position i is a multiple of dc
+        for (int i = E - 1; i >= 1; --i) {
+            const int j = (int)rng.below((uint32_t)i + 1u);
+            const Idx t = S(i);
+            S(i) = S(j);
+            S(j) = t;
+            if (to_check == 0) {
+                to_check = dc;
+                if (!check_ok(i)) { ok = false; break; }
+            }
+            --to_check;
+        }
+        if (ok && !check_ok(0)) ok = false;
+    }
+    return ok;
+}
+
 __global__ __launch_bounds__(64) void sample_regular_kernel(int n, int dv, int dc, uint32_t k0, uint32_t k1,
                                                             uint64_t first_graph, int G, int32_t *check_lookup,
                                                             int32_t *variable_lookup, int32_t *attempts,
@@ -660,47 +697,86 @@ __global__ __launch_bounds__(64) void sample_regular_kernel(int n, int dv, int d
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
     const int E = n * dv;
-    int32_t *seq = check_lookup + (size_t)g * E;
+    int32_t *seq = check_lookup + (size_t)g * E;  // permuted variable ids == check_lookup
     int32_t *vl = variable_lookup + (size_t)g * E;
     const uint64_t gid = first_graph + (uint64_t)g;
     GraphRng rng{k0, k1, (uint32_t)gid, (uint32_t)(gid >> 32)};
-    for (int s = 0; s < E; ++s) seq[s] = s;
+    for (int v = 0, s = 0; v < n; ++v)
+        for (int t = 0; t < dv; ++t) seq[s++] = v;
     int att = 0;
-    bool ok = false;
-    while (!ok && att < max_attempts) {
-        ++att;
-        ok = true;
-        for (int i = E - 1; i >= 1; --i) {
-            const int j = (int)rng.below((uint32_t)i + 1u);
-            const int t = seq[i];
-            seq[i] = seq[j];
-            seq[j] = t;
-            if (i % dc == 0) {  // check i/dc complete
-                for (int x = i; x < i + dc && ok; ++x)
-                    for (int y = x + 1; y < i + dc; ++y)
-                        if (seq[x] / dv == seq[y] / dv) { ok = false; break; }
-                if (!ok) break;
+    const bool ok = sample_one<int32_t>(E, dc, rng, [&](int x) -> int32_t & { return seq[x]; }, max_attempts, att);
+    if (attempts) attempts[g] = ok ? att : -att;
+    // variable_lookup: scanning positions in order fills each row in ascending check order
+    for (int v = 0; v < n; ++v)
+        for (int t = 0; t < dv; ++t) vl[(size_t)v * dv + t] = -1;
+    for (int s = 0, c = 0, r = 0; s < E; ++s) {
+        int32_t *row = vl + (size_t)seq[s] * dv;
+        int k = 0;
+        while (row[k] >= 0) ++k;
+        row[k] = c;
+        if (++r == dc) { r = 0; ++c; }
+    }
+}
+
+// LDS-resident form for n*dv < 65536: each lane of a 64-thread workgroup owns
+// one graph whose permutation lives in LDS as u16 (lane-interleaved); the
+// whole wave then writes the graphs out.  Same draws, same output.
+__global__ __launch_bounds__(64) void sample_regular_lds_kernel(int n, int dv, int dc, uint32_t k0, uint32_t k1,
+                                                                uint64_t first_graph, int G, int per_wg,
+                                                                int32_t *check_lookup, int32_t *variable_lookup,
+                                                                int32_t *attempts, int max_attempts) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int E = n * dv;
+    const int lane = threadIdx.x;
+    const int g0 = blockIdx.x * per_wg;
+    const int ng = min(per_wg, G - g0);
+    uint16_t *seqs = reinterpret_cast<uint16_t *>(smem);  // element x of local graph l at x*per_wg + l
+    for (int x = lane; x < E * per_wg; x += 64) seqs[x] = (uint16_t)((x / per_wg) / dv);
+    __syncthreads();
+    if (lane < ng) {
+        const int l = lane;
+        const uint64_t gid = first_graph + (uint64_t)(g0 + l);
+        GraphRng rng{k0, k1, (uint32_t)gid, (uint32_t)(gid >> 32)};
+        int att = 0;
+        const bool ok = sample_one<uint16_t>(
+            E, dc, rng, [&](int x) -> uint16_t & { return seqs[x * per_wg + l]; }, max_attempts, att);
+        if (attempts) attempts[g0 + l] = ok ? att : -att;
+    }
+    __syncthreads();
+    for (int l = 0; l < ng; ++l) {  // the wave writes graph l out
+        int32_t *chk = check_lookup + (size_t)(g0 + l) * E;
+        for (int x = lane; x < E; x += 64) chk[x] = seqs[x * per_wg + l];
+    }
+    // variable_lookup: claim a row slot per position (atomic CAS on -1), then sort rows
+    for (int l = 0; l < ng; ++l) {
+        int32_t *vl = variable_lookup + (size_t)(g0 + l) * E;
+        for (int x = lane; x < E; x += 64) vl[x] = -1;
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int l = 0; l < ng; ++l) {
+        int32_t *vl = variable_lookup + (size_t)(g0 + l) * E;
+        for (int x = lane; x < E; x += 64) {
+            int32_t *row = vl + (size_t)seqs[x * per_wg + l] * dv;
+            const int c = x / dc;
+            for (int k = 0; k < dv; ++k)
+                if (atomicCAS(&row[k], -1, c) == -1) break;
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int l = 0; l < ng; ++l) {
+        int32_t *vl = variable_lookup + (size_t)(g0 + l) * E;
+        for (int v = lane; v < n; v += 64) {
+            int32_t *r = vl + (size_t)v * dv;
+            for (int x = 1; x < dv; ++x) {
+                const int key = r[x];
+                int y = x - 1;
+                while (y >= 0 && r[y] > key) { r[y + 1] = r[y]; --y; }
+                r[y + 1] = key;
             }
         }
-        if (ok) {  // check 0 completes with the last swap
-            for (int x = 0; x < dc && ok; ++x)
-                for (int y = x + 1; y < dc; ++y)
-                    if (seq[x] / dv == seq[y] / dv) { ok = false; break; }
-        }
     }
-    if (attempts) attempts[g] = ok ? att : -att;
-    // variable_lookup: socket v*dv+t -> its check, then each variable's checks ascending
-    for (int s = 0; s < E; ++s) vl[seq[s]] = s / dc;
-    for (int v = 0; v < n; ++v) {
-        int32_t *r = vl + (size_t)v * dv;
-        for (int x = 1; x < dv; ++x) {  // insertion sort (dv is tiny)
-            const int key = r[x];
-            int y = x - 1;
-            while (y >= 0 && r[y] > key) { r[y + 1] = r[y]; --y; }
-            r[y + 1] = key;
-        }
-    }
-    for (int s = 0; s < E; ++s) seq[s] = seq[s] / dv;  // check_lookup = variable ids
 }
 
 // ===========================================================================
@@ -1083,6 +1159,18 @@ hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t 
                                  int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts,
                                  int max_attempts, hipStream_t stream) {
     if (G <= 0) return hipSuccess;
+    const int E = n * dv;
+    if (E < 65536) {
+        // graphs per workgroup: keep each workgroup's LDS <= 40 KiB (4 workgroups / CU)
+        int per = (int)std::min<long>(64, std::max<long>(1, 40960 / (2L * E)));
+        const size_t lds = (size_t)2 * E * per;
+        hipError_t e = allow_lds(sample_regular_lds_kernel, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(sample_regular_lds_kernel, dim3((G + per - 1) / per), dim3(64), lds, stream, n, dv, dc,
+                           (uint32_t)seed, (uint32_t)(seed >> 32), first_graph, G, per, check_lookup, variable_lookup,
+                           attempts, max_attempts);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(sample_regular_kernel, dim3((G + 63) / 64), dim3(64), 0, stream, n, dv, dc, (uint32_t)seed,
                        (uint32_t)(seed >> 32), first_graph, G, check_lookup, variable_lookup, attempts, max_attempts);
     return hipGetLastError();

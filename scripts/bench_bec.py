@@ -91,5 +91,25 @@ def main():
                           "cpu_baseline": cpu, "kernel": "bec_kernel"}), flush=True)
 
 
+def ensemble(reps=2):
+    """Ensemble mode: a fresh (3,6) graph per trial drawn on the device + decode."""
+    s = torch.cuda.current_stream()
+    for n, eps, iters, B in ((1000, 0.40, 50, 16384), (10000, 0.40, 50, 4096), (64800, 0.40, 200, 1024)):
+        mc = MonteCarlo.ensemble(n, 3, 6, "bec", eps, iters, seed=3, batch=B)
+        mc.run_batch(0, min(B, 256))
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        mc.run_batch(B, B)
+        b.record(s)
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b)
+        print(json.dumps({"workload": f"ensemble (3,6) n={n} eps={eps} {iters} it (graph sampled per trial)",
+                          "batch": B, "trials_per_s": B / ms * 1e3, "ms": ms}), flush=True)
+
+
 if __name__ == "__main__":
+    if "--ensemble" in sys.argv:
+        ensemble()
+        sys.exit(0)
     main()
