@@ -378,3 +378,21 @@ def test_parallel_simulator_ensemble_device(torch, tmp_path, monkeypatch):
                                   message_passing=True, expurgation=2, batch=512))
     assert 0 < res["num_tests"] <= 2000 and res["frame_errors"] <= 200
     assert res["filename"].startswith("regular_code_expurgated=2_BEC=0.45")
+
+
+# ------------------------------------------------------- irregular (config 4)
+@pytest.mark.parametrize("n", [2000, 20000])
+def test_irregular_rsu_vs_oracle(torch, n):
+    """RSU rate-1/2 irregular ensemble: min-sum bit-exact, SPA to tolerance (n=20000 runs the
+    global-scratch kernel: 57k edges do not fit one CU's LDS in fp32)."""
+    from iib_project_ldpc_codes_amd import decoder, ensembles
+    g = ensembles.sample_irregular(ensembles.RSU_DL4, n, seed=5)
+    B = 8
+    llr = oracle.channel(oracle.CH_AWGN, 0.85, 6, 0, n, B)
+    post, hard, its = decoder.bp_decode(g, llr, 20, "minsum", alpha=0.8, early_stop=True)
+    opost, ohard, oits = oracle.bp_decode_batch(g.csr, llr, 20, 1, alpha=0.8, early_stop=True)
+    np.testing.assert_array_equal(post, opost)
+    np.testing.assert_array_equal(its, oits)
+    post, hard, its = decoder.bp_decode(g, llr, 3, "spa")
+    opost, _, _ = oracle.bp_decode_batch(g.csr, llr, 3, 0)
+    np.testing.assert_allclose(post, opost, rtol=SPA_RTOL, atol=SPA_ATOL)
