@@ -310,6 +310,7 @@ struct BpArgs {
     float *scratch;
     // LDS kernel lane layout (ldpc_graph::lane_var / lane_slot)
     const int32_t *lane_var, *lane_slot;
+    int lds_slots;  // generic GMEM kernel: message slots [0, lds_slots) kept in LDS
 };
 
 // ---------------------------------------------------------------------------
@@ -527,10 +528,15 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
     unsigned char *base = GMEM ? reinterpret_cast<unsigned char *>(a.scratch) +
                                      (size_t)blockIdx.x * (((size_t)E * 5 + (size_t)n * 4 + 15) & ~(size_t)15)
                                : smem;
-    float *msg = reinterpret_cast<float *>(base);
-    float *Ls = msg + E;
+    float *msg_all = reinterpret_cast<float *>(base);
+    float *Ls = msg_all + E;
     uint8_t *hs = reinterpret_cast<uint8_t *>(Ls + n);
     int *curve = reinterpret_cast<int *>(GMEM ? smem : smem + (((size_t)E * 5 + (size_t)n * 4 + 15) & ~(size_t)15));
+    // GMEM: the first S message slots live in LDS, the rest in the L2-resident
+    // global slab (generic pointers -> flat loads pick the space per lane).
+    const int S = GMEM ? a.lds_slots : 0;
+    float *msg_lds = reinterpret_cast<float *>(smem + (MC ? (((size_t)(iters + 1) * 4 + 15) & ~(size_t)15) : 0));
+    auto MSG = [&](int e) -> float & { return (GMEM && e < S) ? msg_lds[e] : msg_all[e]; };
 
     for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
         const uint64_t cw = a.first_cw + (uint64_t)b;
@@ -545,7 +551,7 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
             const float l2 = l * Domain<ALGO>::in;
             Ls[v] = l2;
             err0 += (l < 0.0f);
-            for (int e = a.vptr[v]; e < a.vptr[v + 1]; ++e) msg[a.vslot[e]] = l2;
+            for (int e = a.vptr[v]; e < a.vptr[v + 1]; ++e) MSG(a.vslot[e]) = l2;
             if (!MC) {
                 if (a.post) a.post[(size_t)b * n + v] = l;
                 if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(l < 0.0f);
@@ -573,21 +579,21 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
                 const int s0 = a.cptr[c], d = a.cptr[c + 1] - s0;
                 float x[MAXDC];
 #pragma unroll
-                for (int s = 0; s < MAXDC; ++s) x[s] = s < d ? msg[s0 + s] : __builtin_inff();
+                for (int s = 0; s < MAXDC; ++s) x[s] = s < d ? MSG(s0 + s) : __builtin_inff();
                 check_update<ALGO, MAXDC>(x, a.alpha, d);
 #pragma unroll
                 for (int s = 0; s < MAXDC; ++s)
-                    if (s < d) msg[s0 + s] = x[s];
+                    if (s < d) MSG(s0 + s) = x[s];
             }
             __syncthreads();
             int errs = 0;
             for (int v = tid; v < n; v += T) {
                 const int e0 = a.vptr[v], e1 = a.vptr[v + 1];
                 float s = Ls[v];
-                for (int e = e0; e < e1; ++e) s += msg[a.vslot[e]];
+                for (int e = e0; e < e1; ++e) s += MSG(a.vslot[e]);
                 for (int e = e0; e < e1; ++e) {
                     const int sl = a.vslot[e];
-                    msg[sl] = s - msg[sl];
+                    MSG(sl) = s - MSG(sl);
                     if (ET) hs[sl] = (uint8_t)(s < 0.0f);
                 }
                 errs += (s < 0.0f);
@@ -1027,15 +1033,30 @@ hipError_t launch_lds36(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     return hipErrorInvalidValue;
 }
 
+#ifndef LDPC_GMEM_T
+#define LDPC_GMEM_T 1024  // one 1024-thread workgroup per CU ...
+#endif
+#ifndef LDPC_GMEM_GRID
+#define LDPC_GMEM_GRID 256  // ... so the per-workgroup slabs stay cache-resident
+#endif
+#ifndef LDPC_GMEM_HYB
+#define LDPC_GMEM_HYB 1  // first ~38k message slots in LDS, the rest in the slab
+#endif
 template <int MAXDC, int ALGO, bool ET, bool MC, bool GMEM>
 hipError_t launch_generic(const ldpc_graph &g, BpArgs a, hipStream_t s) {
-    constexpr int T = 256;
+    constexpr int T = GMEM ? LDPC_GMEM_T : 256;
     auto k = bp_generic_kernel<T, MAXDC, ALGO, ET, MC, GMEM>;
-    const size_t lds = GMEM ? (MC ? (size_t)(a.max_iters + 1) * 4 : 0) : generic_lds_bytes(g, a.max_iters, MC);
+    size_t lds = GMEM ? (MC ? (((size_t)(a.max_iters + 1) * 4 + 15) & ~(size_t)15) : 0)
+                      : generic_lds_bytes(g, a.max_iters, MC);
+    if (GMEM) {  // fill the rest of the CU's LDS with the first message slots
+        const size_t room = kLdsMax - 4096 - lds;
+        a.lds_slots = LDPC_GMEM_HYB ? (int)std::min<size_t>((size_t)g.E, room / 4) : 0;
+        lds += (size_t)a.lds_slots * 4;
+    }
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
     int grid = a.B;
-    if (GMEM) grid = a.B < 2048 ? a.B : 2048;
+    if (GMEM) grid = a.B < LDPC_GMEM_GRID ? a.B : LDPC_GMEM_GRID;
     hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, s, a);
     return hipGetLastError();
 }
@@ -1093,7 +1114,7 @@ hipError_t launch_bec_decode(const ldpc_graph &g, uint8_t *d_words, int B, int m
 size_t bp_scratch_bytes(const ldpc_graph &g, int B) {
     const size_t per = ((size_t)g.E * 5 + (size_t)g.n * 4 + 15) & ~(size_t)15;
     if (generic_lds_bytes(g, 0, true) + 4096 <= kLdsMax) return 0;
-    const int grid = B < 2048 ? B : 2048;
+    const int grid = B < LDPC_GMEM_GRID ? B : LDPC_GMEM_GRID;
     return per * (size_t)grid;
 }
 
