@@ -83,8 +83,20 @@ def degree_sequences(ens, n):
     return vdeg.astype(np.int32), cdeg.astype(np.int32)
 
 
-def sample_irregular(ens, n, seed=0, max_retries=100000):
-    """Configuration-model graph of ``ens`` with n variables (host, numpy PCG64)."""
+def sample_irregular(ens, n, seed=0, max_retries=100000, deg2="random", min_cycle=40):
+    """Configuration-model graph of ``ens`` with n variables (host, numpy PCG64).
+
+    deg2="random": every socket matched uniformly (the reference's law).  With a
+    large fraction of degree-2 variables this leaves low-weight codewords -- two
+    degree-2 variables on the same two checks, short cycles of degree-2 nodes --
+    and an error floor (FER ~ 1e-1 for RSU_DL4 at n = 20000).
+    deg2="zigzag": the degree-2 variables form a path through a random order of
+    all checks (IRA-style) plus chords whose cycles through the path hold at
+    least ``min_cycle`` degree-2 variables; the other variables are matched
+    uniformly to the remaining check sockets.  Same degree distributions, no
+    degree-2 codeword lighter than ``min_cycle``."""
+    if deg2 == "zigzag":
+        return _sample_zigzag(ens, n, seed, min_cycle, max_retries)
     vdeg, cdeg = degree_sequences(ens, n)
     rng = np.random.default_rng(seed)
     E = int(vdeg.sum())
@@ -106,3 +118,82 @@ def sample_irregular(ens, n, seed=0, max_retries=100000):
     vptr[1:] = np.cumsum(vdeg)
     vslot = order.astype(np.int32)
     return TannerGraph.from_csr(cptr, cvar.astype(np.int32), vptr, vslot)
+
+
+def _csr_from_pairs(n, m, cdeg, var_check_pairs):
+    """CSR slot form from (variable, check) edge pairs; slots check-major, each check's
+    variables in the pair order, each variable's edges in ascending check order."""
+    v = np.asarray([p[0] for p in var_check_pairs], np.int32)
+    c = np.asarray([p[1] for p in var_check_pairs], np.int32)
+    order = np.lexsort((np.arange(v.size), c))  # check-major, stable
+    cvar = v[order]
+    slot_check = c[order]
+    cptr = np.zeros(m + 1, np.int32)
+    cptr[1:] = np.cumsum(np.bincount(c, minlength=m))
+    assert np.array_equal(np.diff(cptr), cdeg)
+    vord = np.lexsort((slot_check, cvar))
+    vptr = np.zeros(n + 1, np.int32)
+    vptr[1:] = np.cumsum(np.bincount(cvar, minlength=n))
+    return TannerGraph.from_csr(cptr, cvar, vptr, vord.astype(np.int32))
+
+
+def _sample_zigzag(ens, n, seed, min_cycle, max_retries):
+    rng = np.random.default_rng(seed)
+    vdeg, cdeg = degree_sequences(ens, n)
+    m = cdeg.size
+    rng.shuffle(cdeg)
+    d2 = np.nonzero(vdeg == 2)[0]
+    others = np.nonzero(vdeg != 2)[0]
+    if d2.size < m - 1:
+        raise ValueError("zigzag needs at least m-1 degree-2 variables")
+    for _ in range(max_retries):
+        order = rng.permutation(m)            # path order of the checks
+        pos = np.empty(m, np.int64)
+        pos[order] = np.arange(m)
+        used = np.zeros(m, np.int64)
+        pairs = []
+        for i in range(m - 1):                # the path: variable d2[i] on checks order[i], order[i+1]
+            a, b = order[i], order[i + 1]
+            pairs += [(d2[i], a), (d2[i], b)]
+            used[a] += 1
+            used[b] += 1
+        chords = []
+        ok = True
+        for v in d2[m - 1:]:                  # chords between far-apart checks with spare sockets
+            for _try in range(1000):
+                a, b = rng.integers(0, m, 2)
+                if used[a] >= cdeg[a] or used[b] >= cdeg[b] or a == b:
+                    continue
+                pa, pb = sorted((pos[a], pos[b]))
+                if pb - pa + 1 < min_cycle:
+                    continue
+                # cycles through two chords: |pa - qa| + |pb - qb| + 2 variables on the cycle
+                if any(abs(pa - qa) + abs(pb - qb) + 2 < min_cycle or abs(pa - qb) + abs(pb - qa) + 2 < min_cycle
+                       for qa, qb in chords):
+                    continue
+                chords.append((pa, pb))
+                pairs += [(v, a), (v, b)]
+                used[a] += 1
+                used[b] += 1
+                break
+            else:
+                ok = False
+                break
+        if not ok:
+            continue
+        # remaining check sockets, matched uniformly to the other variables' sockets
+        rest = np.repeat(np.arange(m), cdeg - used)
+        vs = np.repeat(others, vdeg[others])
+        if rest.size != vs.size:
+            raise RuntimeError("socket count mismatch")
+        for _r in range(max_retries):
+            perm = rng.permutation(rest.size)
+            cs = rest[perm]
+            key = cs.astype(np.int64) * n + vs
+            if np.unique(key).size == key.size:
+                break
+        else:
+            continue
+        pairs += list(zip(vs.tolist(), cs.tolist()))
+        return _csr_from_pairs(n, m, cdeg, pairs)
+    raise RuntimeError("zigzag sampler: too many retries")

@@ -50,3 +50,20 @@ def test_sample_irregular_graph_valid():
     for c in range(0, g.m, 29):
         row = cvar[cptr[c]:cptr[c + 1]]
         assert len(set(row)) == row.size
+
+
+def test_zigzag_construction_preserves_degrees_and_removes_weight2():
+    e = ensembles.RSU_DL4
+    g = ensembles.sample_irregular(e, 4000, seed=2, deg2="zigzag", min_cycle=30)
+    cptr, cvar, vptr, vslot = g.csr
+    vdeg, cdeg = ensembles.degree_sequences(e, 4000)
+    np.testing.assert_array_equal(np.sort(np.diff(vptr)), np.sort(vdeg))
+    np.testing.assert_array_equal(np.sort(np.diff(cptr)), np.sort(cdeg))
+    assert np.array_equal(np.sort(vslot), np.arange(vslot.size))
+    # no two degree-2 variables on the same pair of checks (weight-2 codewords)
+    slot_check = np.repeat(np.arange(g.m), np.diff(cptr))
+    pairs = set()
+    for v in np.nonzero(np.diff(vptr) == 2)[0]:
+        p = tuple(sorted(slot_check[vslot[vptr[v]:vptr[v + 1]]]))
+        assert p not in pairs
+        pairs.add(p)
