@@ -52,10 +52,12 @@ class TannerGraph:
         return cls(np.array(var, np.int32), np.array(check, np.int32), n, n - m, dv, dc)
 
     @classmethod
-    def random_regular(cls, n, dv, dc, seed=0, max_retries=10000):
+    def random_regular(cls, n, dv, dc, seed=0, max_retries=10000, distinct_columns=False):
         """Configuration-model (dv, dc) graph with the law of random_code_generator.c:21-67:
         uniform socket permutation, check_lookup[i] = socket // dv, whole-graph redraw
         whenever a check holds a variable twice, variable_lookup in ascending check order.
+        distinct_columns=True also redraws graphs with two identical columns (weight-2
+        codewords), as random_code_generator_python.py:4-54 does.
         Randomness: numpy PCG64 seeded by ``seed`` (the reference uses libc rand())."""
         k = int(n * (dc - dv) / dc)
         m = n - k
@@ -70,6 +72,8 @@ class TannerGraph:
             checks = np.repeat(np.arange(m, dtype=np.int32), dc)
             order = np.lexsort((checks, chk))  # by variable, then ascending check
             var = checks[order].astype(np.int32)
+            if distinct_columns and np.unique(var.reshape(n, dv), axis=0).shape[0] != n:
+                continue
             return cls(var, chk, n, k, dv, dc)
         raise RuntimeError("random_regular: too many redraws")
 

@@ -1,0 +1,73 @@
+"""FER / BER waterfall sweeps on the device Monte-Carlo engine (configs[2] and configs[3]).
+
+  cfg3: (3,6) n=10000, BSC, normalized min-sum, crossover sweep, ~1M trials per point
+  cfg4: RSU rate-1/2 irregular (zigzag degree-2 placement), n=20000, BI-AWGN, SPA, 100 it
+One process per GPU (torchrun); trials shard by index, counters all-reduced per round.
+Each point stops at 200 frame errors (parallel_simulator.py:198), --trials, or --seconds.
+
+  python scripts/fer_sweep.py cfg3 [--trials 1000000] [--seconds 60]
+  torchrun --nproc-per-node 8 scripts/fer_sweep.py cfg4 --seconds 300
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from iib_project_ldpc_codes_amd import de, ensembles  # noqa: E402
+from iib_project_ldpc_codes_amd.graph import TannerGraph  # noqa: E402
+from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("config", choices=["cfg3", "cfg4"])
+    ap.add_argument("--trials", type=int, default=1_000_000)
+    ap.add_argument("--seconds", type=float, default=60.0)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--points", type=str, default=None)
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+    if world > 1:
+        dist.init_process_group("nccl")
+    rank = dist.get_rank() if world > 1 else 0
+    if args.config == "cfg3":
+        g = TannerGraph.random_regular(10000, 3, 6, seed=1, distinct_columns=True)
+        channel, algo, alpha, iters = "bsc", "minsum", 0.75, 50
+        points = [float(p) for p in (args.points or "0.07,0.065,0.06,0.055,0.05").split(",")]
+        batch = args.batch or 65536
+    else:
+        g = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1, deg2="zigzag")
+        channel, algo, alpha, iters = "awgn", "spa", 1.0, 100
+        points = [float(p) for p in (args.points or "0.86,0.84,0.82,0.80,0.78").split(",")]
+        batch = args.batch or 16384
+    rate = 1.0 - g.m / g.n
+    for p in points:
+        mc = MonteCarlo(g, channel, p, iters, algo=algo, alpha=alpha, early_stop=True, seed=11, batch=batch)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        res = mc.run(num_tests=args.trials, stop_frame_errors=200, time_limit=args.seconds)
+        torch.cuda.synchronize()
+        el = time.time() - t0
+        if rank == 0:
+            out = {"config": args.config, "channel": channel, "param": p, "algo": algo, "iterations": iters,
+                   "n": g.n, "rate": rate, "gpus": world, "trials": res["num_tests"],
+                   "frame_errors": res["frame_errors"], "fer": res["fer"], "ber": res["ber"],
+                   "mean_iterations": res["iterations"] / max(res["num_tests"], 1),
+                   "seconds": el, "codewords_per_s": res["num_tests"] / el}
+            if channel == "awgn":
+                out["ebn0_db"] = float(de.sigma_to_ebn0_db(p, rate))
+            print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
