@@ -39,7 +39,7 @@ struct DevBuf {
 };
 
 struct Workspace {
-    DevBuf trial, its, cutoff, scratch, words, llr, post, hard, errors, itsb, gchk, gvar, gatt;
+    DevBuf trial, its, cutoff, scratch, words, llr, post, hard, errors, itsb, gchk, gvar, gatt, mlw, mlo, mlu;
 };
 std::map<std::pair<int, void *>, Workspace> g_ws;  // (device, stream)
 
@@ -704,6 +704,124 @@ int ldpc_mc_ensemble_batch_dev(int n, int dv, int dc, int channel, float param, 
     LDPC_HIP(launch_mc_bec_ensemble(n, dv, dc, chk, var, p, seed, first_cw, B, max_iters, trial, its, s));
     LDPC_HIP(launch_mc_reduce(trial, its, B, max_iters, expurgation, stop_frame_errors, d_counters,
                               static_cast<int32_t *>(ws.cutoff.p), s));
+    return LDPC_OK;
+}
+
+// --------------------------- ML ("optimal") erasure decoding ---------------
+static int ml_check_shape(int n, int m) {
+    LDPC_REQUIRE(m >= 1 && m <= 1000, "ML decoding supports 1 <= n-k <= 1000 checks");
+    LDPC_REQUIRE(n >= 1 && n <= 32767, "ML decoding supports n <= 32767");
+    return LDPC_OK;
+}
+
+int ldpc_ml_decode_batch_dev(const ldpc_graph *g, const uint8_t *d_words, int B, uint8_t *d_out,
+                             int32_t *d_unsolved, void *stream) {
+    LDPC_REQUIRE(g && d_words && d_out && d_unsolved && B >= 0, "bad ML batch arguments");
+    int rc = ml_check_shape(g->n, g->m);
+    if (rc) return rc;
+    if (B == 0) return LDPC_OK;
+    LDPC_HIP(launch_ml_decode(g->cptr, g->cvar, 0, 0, g->n, g->m, d_words, B, d_out, d_unsolved,
+                              static_cast<hipStream_t>(stream)));
+    return LDPC_OK;
+}
+
+int ldpc_ml_decode_batch(const ldpc_graph *g, const uint8_t *words, int B, uint8_t *out, int32_t *unsolved) {
+    LDPC_REQUIRE(g && words && out && unsolved && B >= 0, "bad ML batch arguments");
+    int rc = ml_check_shape(g->n, g->m);
+    if (rc) return rc;
+    if (B == 0) return LDPC_OK;
+    const size_t bytes = (size_t)B * g->n;
+    std::lock_guard<std::mutex> lk(g_mu);
+    Workspace &ws = workspace(nullptr);
+    LDPC_HIP(ws.mlw.ensure(bytes));
+    LDPC_HIP(ws.mlo.ensure(bytes));
+    LDPC_HIP(ws.mlu.ensure(sizeof(int32_t) * (size_t)B));
+    uint8_t *dw = static_cast<uint8_t *>(ws.mlw.p), *dout = static_cast<uint8_t *>(ws.mlo.p);
+    int32_t *du = static_cast<int32_t *>(ws.mlu.p);
+    LDPC_HIP(hipMemcpy(dw, words, bytes, hipMemcpyHostToDevice));
+    LDPC_HIP(launch_ml_decode(g->cptr, g->cvar, 0, 0, g->n, g->m, dw, B, dout, du, nullptr));
+    LDPC_HIP(hipDeviceSynchronize());
+    LDPC_HIP(hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost));
+    LDPC_HIP(hipMemcpy(unsolved, du, sizeof(int32_t) * (size_t)B, hipMemcpyDeviceToHost));
+    return LDPC_OK;
+}
+
+int ldpc_ml_ensemble_decode_dev(int n, int dv, int dc, const int32_t *d_check_lookup, const uint8_t *d_words, int B,
+                                uint8_t *d_out, int32_t *d_unsolved, void *stream) {
+    int rc = check_regular_shape(n, dv, dc);
+    if (rc) return rc;
+    LDPC_REQUIRE(d_check_lookup && d_words && d_out && d_unsolved && B >= 0, "bad ML batch arguments");
+    rc = ml_check_shape(n, n * dv / dc);
+    if (rc) return rc;
+    rc = require_device();
+    if (rc) return rc;
+    if (B == 0) return LDPC_OK;
+    LDPC_HIP(launch_ml_decode(nullptr, d_check_lookup, (int64_t)n * dv, dc, n, n * dv / dc, d_words, B, d_out,
+                              d_unsolved, static_cast<hipStream_t>(stream)));
+    return LDPC_OK;
+}
+
+int ldpc_mc_ml_batch_dev(const ldpc_graph *g, int n, int dv, int dc, float eps, uint64_t seed, uint64_t first_cw,
+                         int B, int max_iters, int message_passing, int expurgation, int64_t stop_frame_errors,
+                         int64_t *d_counters_mp, int64_t *d_counters_ml, void *stream) {
+    LDPC_REQUIRE(d_counters_ml && B >= 0 && max_iters >= 0, "bad MC arguments");
+    LDPC_REQUIRE(!message_passing || d_counters_mp, "message_passing needs d_counters_mp");
+    float p, p2;
+    int rc = channel_params(LDPC_CH_BEC, eps, &p, &p2);
+    if (rc) return rc;
+    const bool ens = (g == nullptr);
+    if (ens) {
+        rc = check_regular_shape(n, dv, dc);
+        if (rc) return rc;
+        rc = require_device();
+        if (rc) return rc;
+    } else {
+        n = g->n;
+    }
+    const int m = ens ? n * dv / dc : g->m;
+    rc = ml_check_shape(n, m);
+    if (rc) return rc;
+    if (B == 0) return LDPC_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(g_mu);
+    Workspace &ws = workspace(stream);
+    LDPC_HIP(ws.mlw.ensure((size_t)B * n));
+    LDPC_HIP(ws.mlo.ensure((size_t)B * n));
+    LDPC_HIP(ws.mlu.ensure(sizeof(int32_t) * (size_t)B));
+    LDPC_HIP(ws.cutoff.ensure(16));
+    uint8_t *dw = static_cast<uint8_t *>(ws.mlw.p), *dout = static_cast<uint8_t *>(ws.mlo.p);
+    int32_t *du = static_cast<int32_t *>(ws.mlu.p), *cut = static_cast<int32_t *>(ws.cutoff.p);
+    int32_t *chk = nullptr, *var = nullptr;
+    if (ens) {
+        const size_t E = (size_t)n * dv;
+        LDPC_HIP(ws.gchk.ensure(E * B * 4));
+        LDPC_HIP(ws.gvar.ensure(E * B * 4));
+        chk = static_cast<int32_t *>(ws.gchk.p);
+        var = static_cast<int32_t *>(ws.gvar.p);
+        LDPC_HIP(launch_sample_regular(n, dv, dc, seed, first_cw, B, chk, var, nullptr, 1 << 20, s));
+    }
+    // channel words of trials first_cw.. (the same Philox draws the fused BP kernels make)
+    LDPC_HIP(launch_channel(LDPC_CH_BEC, p, p2, seed, first_cw, n, B, dw, s));
+    if (ens)
+        LDPC_HIP(launch_ml_decode(nullptr, chk, (int64_t)n * dv, dc, n, m, dw, B, dout, du, s));
+    else
+        LDPC_HIP(launch_ml_decode(g->cptr, g->cvar, 0, 0, n, m, dw, B, dout, du, s));
+    if (message_passing) {
+        LDPC_HIP(ws.trial.ensure(sizeof(int32_t) * (size_t)B * (max_iters + 1)));
+        LDPC_HIP(ws.its.ensure(sizeof(int32_t) * (size_t)B));
+        int32_t *trial = static_cast<int32_t *>(ws.trial.p), *its = static_cast<int32_t *>(ws.its.p);
+        if (ens)
+            LDPC_HIP(launch_mc_bec_ensemble(n, dv, dc, chk, var, p, seed, first_cw, B, max_iters, trial, its, s));
+        else
+            LDPC_HIP(launch_mc_decode(*g, LDPC_CH_BEC, p, p2, seed, first_cw, B, max_iters, 0, 1.0f, 0, trial, its,
+                                      s, nullptr));
+        // the stop rule counts message-passing frame errors (parallel_simulator.py:226-231)
+        LDPC_HIP(launch_mc_reduce(trial, its, B, max_iters, expurgation, stop_frame_errors, d_counters_mp, cut, s));
+        LDPC_HIP(launch_mc_reduce_cut(du, nullptr, B, 0, -1, cut, d_counters_ml, s));
+    } else {
+        // ML only: the stop rule counts ML frame errors (:240-241)
+        LDPC_HIP(launch_mc_reduce(du, nullptr, B, 0, -1, stop_frame_errors, d_counters_ml, cut, s));
+    }
     return LDPC_OK;
 }
 

@@ -90,6 +90,15 @@ hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lo
                                   float p, uint64_t seed, uint64_t first_cw, int B, int max_iters, int32_t *trial,
                                   int32_t *trial_its, hipStream_t stream);
 
+// ML ("optimal") erasure decoding, one workgroup per word (m <= 1000).
+// cptr == nullptr: regular lists (check c = slots [c*dc, c*dc+dc)), word b reads
+// cvar + b*cvar_stride.
+hipError_t launch_ml_decode(const int32_t *cptr, const int32_t *cvar, int64_t cvar_stride, int dc, int n, int m,
+                            const uint8_t *d_in, int B, uint8_t *d_out, int32_t *d_unsolved, hipStream_t stream);
+// mc_reduce with a cutoff computed by an earlier launch_mc_reduce (trial_its may be null).
+hipError_t launch_mc_reduce_cut(const int32_t *trial, const int32_t *trial_its, int B, int max_iters, int expurgation,
+                                const int32_t *d_cutoff, int64_t *d_counters, hipStream_t stream);
+
 // Kernel-choice introspection for tests / bench ("lds36", "generic", ...).
 const char *bp_kernel_name(const ldpc_graph &g, int early_stop);
 

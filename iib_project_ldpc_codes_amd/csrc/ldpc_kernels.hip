@@ -6,6 +6,7 @@
 //   message_passing.c:7-82         -> bec_kernel           (bit-exact)
 //   channels.py:24-26 new_transmit -> channel_kernel / chan_* (same law, Philox)
 //   parallel_simulator.py:198-244  -> mc_* (per-trial statistics + stop rule)
+//   parallel_simulator.py:60-129   -> ml_kernel (ML erasure decoding, optimal_decode)
 #include <rocrand/rocrand_kernel.h>
 
 #include <algorithm>
@@ -427,21 +428,19 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 
         int it = 0;
         for (; it < iters; ++it) {
-            if (ET && it > 0) {  // syndrome of the previous iteration's hard decision
-                int unsat = 0;
-                for (int c = tid; c < m; c += T) {
+            if (it > 0) __syncthreads();  // variable phase (msg, hs) complete
+            // check phase; with ET it also evaluates the syndrome of the previous
+            // iteration's hard decisions, and the decoder stops before the next
+            // variable phase when every check is satisfied
+            int unsat = 0;
+#pragma unroll LDPC_CHECK_UNROLL
+            for (int c = tid; c < m; c += T) {
+                if (ET && it > 0) {
                     int par = 0;
 #pragma unroll
                     for (int s = 0; s < DC; ++s) par ^= hs[c * DC + s];
                     unsat |= par;
                 }
-                if (!__syncthreads_or(unsat)) break;
-            } else if (it > 0) {
-                __syncthreads();
-            }
-            // check phase
-#pragma unroll LDPC_CHECK_UNROLL
-            for (int c = tid; c < m; c += T) {
                 float x[DC];
                 if constexpr (DC % 2 == 0) {
                     const float2 *p = reinterpret_cast<const float2 *>(msg + c * DC);
@@ -470,7 +469,11 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     for (int s = 0; s < DC; ++s) msg[c * DC + s] = x[s];
                 }
             }
-            __syncthreads();
+            if constexpr (ET) {
+                if (!__syncthreads_or(unsat | (it == 0))) break;
+            } else {
+                __syncthreads();
+            }
             // Launder the packed slots so the compiler cannot hoist their
             // unpacking out of the iteration loop (VPT*DV pinned addresses spill).
 #pragma unroll
@@ -564,19 +567,15 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
         __syncthreads();
         int it = 0;
         for (; it < iters; ++it) {
-            if (ET && it > 0) {
-                int unsat = 0;
-                for (int c = tid; c < m; c += T) {
-                    int par = 0;
-                    for (int s = a.cptr[c]; s < a.cptr[c + 1]; ++s) par ^= hs[s];
-                    unsat |= par;
-                }
-                if (!__syncthreads_or(unsat)) break;
-            } else if (it > 0) {
-                __syncthreads();
-            }
+            if (it > 0) __syncthreads();  // variable phase (messages, hs) complete
+            int unsat = 0;                // ET: syndrome of the previous hard decisions
             for (int c = tid; c < m; c += T) {
                 const int s0 = a.cptr[c], d = a.cptr[c + 1] - s0;
+                if (ET && it > 0) {
+                    int par = 0;
+                    for (int s = 0; s < d; ++s) par ^= hs[s0 + s];
+                    unsat |= par;
+                }
                 float x[MAXDC];
 #pragma unroll
                 for (int s = 0; s < MAXDC; ++s) x[s] = s < d ? MSG(s0 + s) : __builtin_inff();
@@ -585,7 +584,11 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
                 for (int s = 0; s < MAXDC; ++s)
                     if (s < d) MSG(s0 + s) = x[s];
             }
-            __syncthreads();
+            if constexpr (ET) {
+                if (!__syncthreads_or(unsat | (it == 0))) break;
+            } else {
+                __syncthreads();
+            }
             int errs = 0;
             for (int v = tid; v < n; v += T) {
                 const int e0 = a.vptr[v], e1 = a.vptr[v + 1];
@@ -902,7 +905,7 @@ __global__ __launch_bounds__(256) void mc_reduce_kernel(const int32_t *trial, co
             fr += (f != 0);
             bits += f;
         }
-        itn += its[b];
+        itn += its ? its[b] : 0;
     }
     long long v[3] = {fr, bits, itn};
 #pragma unroll
@@ -923,6 +926,242 @@ __global__ __launch_bounds__(256) void mc_reduce_kernel(const int32_t *trial, co
         atomicAdd(c + 2, (unsigned long long)s[1]);
         atomicAdd(c + 3, (unsigned long long)s[2]);
     }
+}
+
+// ===========================================================================
+// 6. ML ("optimal") erasure decoding -- optimal_decode, parallel_simulator.py:60-129
+//    (system set-up of ml_decoder.c:7-36, GF(2) row_reduce of the galois package)
+// ===========================================================================
+//
+// One workgroup per word.  Thread t holds ROW POSITION t of the augmented system
+// [A | target] in registers as W 64-bit words (A = H restricted to the erased
+// columns that are still unknown, target = parity of the known 1-bits of each
+// active check), so elimination needs no LDS for the matrix: per column j one
+// ballot + LDS atomicMin finds the pivot row (first position >= j with bit j set,
+// galois' choice), the pivot row is broadcast through LDS (double-buffered by
+// column parity, two barriers per column), rows p and q swap through LDS, and
+// every other row holding bit j XORs the pivot in (Gauss-Jordan, above and below).
+// Because the reference looks for the FIRST column whose diagonal entry of the
+// reduced matrix is not 1, elimination stops at the first column without a pivot
+// (all earlier columns are pivots, so that column IS the first diagonal miss):
+// that unknown is given up, every check holding it is dropped, and the system is
+// rebuilt from the graph and reduced again -- the reference's loop (:93-108).
+// When every remaining column has a pivot the solution is read off the augmented
+// bit of rows 0..ncols-1 (:110-121).  Words with no erasure or more erasures than
+// checks are returned unchanged (:66-70).  m <= 1000 (the 1000-unknown cap of
+// :96 can then never bind); n <= 32767.
+//
+// Per-word LDS (dynamic): piv[2][W], swp[W] (u64); best[2], wsum[16] (int);
+// code[n] (int16: column of an active unknown, -1/-2 known 0/1, -3 given up);
+// state[n] (u8: 0/1 known, 2 unknown, 3 given up, 4/5 solved 0/1);
+// rowchk[m], colvar[m] (int16); achk[m] (u8).
+
+__device__ __forceinline__ int ml_block_scan(int x, int *wsum, int &total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int incl = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int w = 0; w < nw; ++w) {
+        const int v = wsum[w];
+        base += (w < wave) ? v : 0;
+        tot += v;
+    }
+    __syncthreads();
+    total = tot;
+    return base + incl - x;
+}
+
+// Register-array helpers with static indices only (a data-dependent index would
+// push R[] to scratch): set bit k by masks, and drop the front word (the
+// elimination window: columns left of the current 64-column block are never read
+// again, and every row's bit j sits in word 0).
+template <int W>
+__device__ __forceinline__ void ml_set_bit(uint64_t (&R)[W], int k) {
+    const int kw = k >> 6;
+    const uint64_t b = 1ull << (k & 63);
+#pragma unroll
+    for (int w = 0; w < W; ++w) R[w] |= (0ull - (uint64_t)(kw == w)) & b;
+}
+
+template <int W>
+__device__ __forceinline__ void ml_shift(uint64_t (&R)[W]) {
+#pragma unroll
+    for (int w = 0; w + 1 < W; ++w) R[w] = R[w + 1];
+    R[W - 1] = 0;
+}
+
+// cptr == nullptr: regular lists, check c owns slots [c*dc, c*dc+dc) of
+// cvar + b*cvar_stride (ensemble mode: word b decodes on its own graph b).
+template <int W>
+__global__ __launch_bounds__(1024) void ml_kernel(const int32_t *__restrict__ cptr, const int32_t *__restrict__ cvar,
+                                                  int64_t cvar_stride, int dc, int n, int m,
+                                                  const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                                                  int32_t *__restrict__ unsolved) {
+    extern __shared__ __align__(16) unsigned char ml_lds[];
+    uint64_t *piv = reinterpret_cast<uint64_t *>(ml_lds);  // [2][W]
+    uint64_t *swp = piv + 2 * W;                            // [W]
+    int *best = reinterpret_cast<int *>(swp + W);           // [2]
+    int *wsum = best + 2;                                   // [16]
+    int16_t *code = reinterpret_cast<int16_t *>(wsum + 16); // [n]
+    int16_t *rowchk = code + n;                             // [m]
+    int16_t *colvar = rowchk + m;                           // [m]
+    uint8_t *state = reinterpret_cast<uint8_t *>(colvar + m);  // [n]
+    uint8_t *achk = state + n;                              // [m]
+
+    const int tid = threadIdx.x, T = blockDim.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const size_t b = blockIdx.x;
+    const uint8_t *w_in = in + b * n;
+    uint8_t *w_out = out + b * n;
+    const int32_t *gv = cvar + (int64_t)b * cvar_stride;
+
+    int ne_local = 0;
+    for (int v = tid; v < n; v += T) {
+        const uint8_t x = w_in[v];
+        state[v] = x == 2 ? 2 : (x ? 1 : 0);
+        ne_local += (x == 2);
+    }
+    for (int c = tid; c < m; c += T) achk[c] = 1;
+    if (tid < 2) best[tid] = INT_MAX;
+    int ne = 0;
+    (void)ml_block_scan(ne_local, wsum, ne);  // (its barriers also publish state / achk / best)
+    if (ne == 0 || ne > m) {
+        for (int v = tid; v < n; v += T) w_out[v] = w_in[v];
+        if (tid == 0) unsolved[b] = ne;
+        return;
+    }
+    const int vper = (n + T - 1) / T, cper = (m + T - 1) / T;
+    int marks = 0;
+    for (;;) {
+        // --- columns: the active unknowns in position order
+        const int v0 = min(n, tid * vper), v1 = min(n, v0 + vper);
+        int cnt = 0;
+        for (int v = v0; v < v1; ++v) cnt += (state[v] == 2);
+        int ncols = 0;
+        int col = ml_block_scan(cnt, wsum, ncols);
+        for (int v = v0; v < v1; ++v) {
+            const int st = state[v];
+            if (st == 2) {
+                colvar[col] = (int16_t)v;
+                code[v] = (int16_t)col++;
+            } else {
+                code[v] = (int16_t)(st == 3 ? -3 : -1 - st);
+            }
+        }
+        // --- rows: the active checks in index order
+        const int c0 = min(m, tid * cper), c1 = min(m, c0 + cper);
+        cnt = 0;
+        for (int c = c0; c < c1; ++c) cnt += achk[c];
+        int nrows = 0;
+        int pos = ml_block_scan(cnt, wsum, nrows);  // barrier: code[] / colvar[] complete
+        for (int c = c0; c < c1; ++c)
+            if (achk[c]) rowchk[pos++] = (int16_t)c;
+        __syncthreads();
+        // --- build row `tid` of [A | target]
+        uint64_t R[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) R[w] = 0;
+        int s_lo = 0, s_hi = 0;
+        if (tid < nrows) {
+            const int c = rowchk[tid];
+            s_lo = cptr ? cptr[c] : c * dc;
+            s_hi = cptr ? cptr[c + 1] : s_lo + dc;
+            int tgt = 0;
+            for (int s = s_lo; s < s_hi; ++s) {
+                const int v = gv[s];
+                const int k = code[v];
+                if (k >= 0) {
+                    ml_set_bit<W>(R, k);  // H is a 0/1 matrix: set, not toggle
+                } else if (k == -2) {
+                    bool dup = false;     // a variable listed twice in a check counts once
+                    for (int s2 = s_lo; s2 < s; ++s2) dup |= (gv[s2] == v);
+                    tgt ^= dup ? 0 : 1;
+                }
+            }
+            if (tgt) ml_set_bit<W>(R, ncols);
+        }
+        // --- Gauss-Jordan in galois' pivot order until the first column without a pivot.
+        // Window: R[0] holds columns [64*shift, 64*shift+64) of the row.
+        int free_col = -1, shift = 0;
+        for (int j = 0; j < ncols; ++j) {
+            const int buf = j & 1;
+            if ((j >> 6) != shift) {
+                ml_shift<W>(R);
+                ++shift;
+            }
+            const int live = W - shift;  // words still in the window (uniform)
+            const bool bit = (R[0] >> (j & 63)) & 1ull;
+            const uint64_t bal = __ballot(bit && tid >= j && tid < nrows);
+            if (lane == 0 && bal) atomicMin(&best[buf], wave * 64 + (int)__ffsll((long long)bal) - 1);
+            __syncthreads();
+            const int q = best[buf];
+            if (tid == 0) best[buf ^ 1] = INT_MAX;
+            if (q == INT_MAX) {
+                free_col = j;
+                break;
+            }
+            uint64_t *pb = piv + buf * W;
+            if (tid == q) {
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    if (w < live) pb[w] = R[w];
+            } else if (tid == j) {
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    if (w < live) swp[w] = R[w];
+            }
+            __syncthreads();
+            if (tid == q) {
+                if (q != j) {
+#pragma unroll
+                    for (int w = 0; w < W; ++w)
+                        if (w < live) R[w] = swp[w];
+                }
+            } else if (tid == j) {
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    if (w < live) R[w] = pb[w];
+            } else if (bit) {
+#pragma unroll
+                for (int w = 0; w < W; ++w)
+                    if (w < live) R[w] ^= pb[w];
+            }
+        }
+        if (free_col < 0) {
+            // full column rank: unknown j = augmented bit (column ncols) of row j
+            while (shift < (ncols >> 6)) {
+                ml_shift<W>(R);
+                ++shift;
+            }
+            if (tid < ncols) {
+                const int v = colvar[tid];
+                state[v] = (uint8_t)(4 + ((R[0] >> (ncols & 63)) & 1ull));
+            }
+            __syncthreads();
+            break;
+        }
+        // --- give the unknown up: drop it and every check that holds it
+        const int vf = colvar[free_col];
+        if (tid < nrows) {
+            bool has = false;
+            for (int s = s_lo; s < s_hi; ++s) has |= (gv[s] == vf);
+            if (has) achk[rowchk[tid]] = 0;
+        }
+        if (tid == 0) state[vf] = 3;
+        ++marks;
+        __syncthreads();
+    }
+    for (int v = tid; v < n; v += T) {
+        const int st = state[v];
+        w_out[v] = st == 3 ? 2 : (st >= 4 ? (uint8_t)(st - 4) : w_in[v]);
+    }
+    if (tid == 0) unsolved[b] = marks;
 }
 
 // ===========================================================================
@@ -1226,6 +1465,51 @@ hipError_t launch_mc_reduce(const int32_t *trial, const int32_t *trial_its, int 
                        stop_frame_errors, d_counters, d_cutoff);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    const int blocks = B < 1024 ? (B + 63) / 64 : 256;
+    hipLaunchKernelGGL(mc_reduce_kernel, dim3(blocks), dim3(256), 0, stream, trial, trial_its, B, max_iters,
+                       expurgation, d_cutoff, d_counters);
+    return hipGetLastError();
+}
+
+size_t ml_lds_bytes(int n, int m, int W) {
+    return (size_t)8 * 3 * W + 4 * 18 + (size_t)2 * n + (size_t)4 * m + (size_t)n + (size_t)m + 16;
+}
+
+int ml_words(int m) {
+    const int need = (m + 1 + 63) / 64;
+    for (int w : {1, 2, 4, 8, 16})
+        if (w >= need) return w;
+    return 0;
+}
+
+hipError_t launch_ml_decode(const int32_t *cptr, const int32_t *cvar, int64_t cvar_stride, int dc, int n, int m,
+                            const uint8_t *d_in, int B, uint8_t *d_out, int32_t *d_unsolved, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    const int W = ml_words(m);
+    const int T = std::min(1024, std::max(64, (m + 63) / 64 * 64));
+    const size_t lds = ml_lds_bytes(n, m, W);
+#define LDPC_ML_CASE(WW)                                                                                    \
+    case WW: {                                                                                              \
+        hipError_t e = allow_lds(ml_kernel<WW>, lds);                                                       \
+        if (e != hipSuccess) return e;                                                                      \
+        hipLaunchKernelGGL(ml_kernel<WW>, dim3(B), dim3(T), lds, stream, cptr, cvar, cvar_stride, dc, n, m, \
+                           d_in, d_out, d_unsolved);                                                        \
+        return hipGetLastError();                                                                           \
+    }
+    switch (W) {
+        LDPC_ML_CASE(1)
+        LDPC_ML_CASE(2)
+        LDPC_ML_CASE(4)
+        LDPC_ML_CASE(8)
+        LDPC_ML_CASE(16)
+        default: return hipErrorInvalidValue;
+    }
+#undef LDPC_ML_CASE
+}
+
+hipError_t launch_mc_reduce_cut(const int32_t *trial, const int32_t *trial_its, int B, int max_iters, int expurgation,
+                                const int32_t *d_cutoff, int64_t *d_counters, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
     const int blocks = B < 1024 ? (B + 63) / 64 : 256;
     hipLaunchKernelGGL(mc_reduce_kernel, dim3(blocks), dim3(256), 0, stream, trial, trial_its, B, max_iters,
                        expurgation, d_cutoff, d_counters);

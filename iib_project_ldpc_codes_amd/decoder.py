@@ -2,6 +2,8 @@
 
 * ``bec_decode``  -- message_passing.c:7-82 over a batch of words (bit-exact).
 * ``bp_decode``   -- flooding sum-product / normalized min-sum (new capability).
+* ``ml_decode``   -- ML ("optimal") erasure decoding, optimal_decode of
+                     parallel_simulator.py:60-129 (GF(2) elimination on the device).
 * ``channel``     -- on-device BEC / BSC / BI-AWGN channel outputs (Philox).
 
 Device forms take torch CUDA(HIP) tensors and run asynchronously on the
@@ -73,6 +75,52 @@ def bec_decode(graph, words, max_iters, errors=None):
                                              err.ctypes.data, its.ctypes.data)
     _native.check(rc, "ldpc_bec_decode_batch")
     return w, err, its
+
+
+# ------------------------------------------------------------------------ ML
+def ml_decode_dev(graph, words, out=None, unsolved=None, stream=None):
+    """words: uint8 [B, n] device tensor (0/1 known, 2 erased).  Returns (out, unsolved):
+    decoded words with 2 where the reference's loop gives an unknown up, and the
+    number of 2s per word (parallel_simulator.py:60-129, :235)."""
+    torch = _torch()
+    assert words.dtype == torch.uint8 and words.is_contiguous() and words.shape[1] == graph.n
+    B = words.shape[0]
+    if out is None:
+        out = torch.empty_like(words)
+    if unsolved is None:
+        unsolved = torch.empty((B,), dtype=torch.int32, device=words.device)
+    rc = _native.lib().ldpc_ml_decode_batch_dev(graph.handle(), words.data_ptr(), B, out.data_ptr(),
+                                                unsolved.data_ptr(), _stream(stream))
+    _native.check(rc, "ldpc_ml_decode_batch_dev")
+    return out, unsolved
+
+
+def ml_decode(graph, words):
+    """Host form: words uint8 [B, n] numpy.  Returns (out, unsolved) numpy."""
+    w = np.ascontiguousarray(np.atleast_2d(words), dtype=np.uint8)
+    B = w.shape[0]
+    out = np.zeros_like(w)
+    uns = np.zeros(B, np.int32)
+    rc = _native.lib().ldpc_ml_decode_batch(graph.handle(), w.ctypes.data, B, out.ctypes.data, uns.ctypes.data)
+    _native.check(rc, "ldpc_ml_decode_batch")
+    return out, uns
+
+
+def ml_ensemble_decode_dev(n, dv, dc, check_lookup, words, out=None, unsolved=None, stream=None):
+    """Word b decoded on graph b: check_lookup int32 [B, n*dv] device tensor
+    (graph.sample_device / ldpc_sample_regular_dev layout)."""
+    torch = _torch()
+    B = words.shape[0]
+    assert check_lookup.dtype == torch.int32 and check_lookup.is_contiguous()
+    assert tuple(check_lookup.shape) == (B, n * dv) and words.dtype == torch.uint8 and words.shape[1] == n
+    if out is None:
+        out = torch.empty_like(words)
+    if unsolved is None:
+        unsolved = torch.empty((B,), dtype=torch.int32, device=words.device)
+    rc = _native.lib().ldpc_ml_ensemble_decode_dev(n, dv, dc, check_lookup.data_ptr(), words.data_ptr(), B,
+                                                   out.data_ptr(), unsolved.data_ptr(), _stream(stream))
+    _native.check(rc, "ldpc_ml_ensemble_decode_dev")
+    return out, unsolved
 
 
 # ---------------------------------------------------------------------- soft

@@ -47,6 +47,25 @@ def ensemble_executor(mc, n, dv, dc):
     return run
 
 
+def ml_executor(mc):
+    """Batch executor of the "optimal" modes (ldpc_mc_ml_batch_dev): ML decoding of each
+    trial's BEC word, plus message passing on the same word when mc.message_passing."""
+    torch = mc.torch
+    ens = isinstance(mc.graph, _Ensemble)
+
+    def run(first_cw, B, stop_frame_errors, counters, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream()
+        g = mc.graph
+        rc = _native.lib().ldpc_mc_ml_batch_dev(None if ens else g.handle(), g.n, g.dv if ens else 0,
+                                                g.dc if ens else 0, mc.param, mc.seed, int(first_cw), int(B),
+                                                mc.max_iters, int(mc.message_passing), mc.expurgation,
+                                                int(stop_frame_errors),
+                                                counters.data_ptr() if mc.message_passing else None,
+                                                mc.counters_ml.data_ptr(), s.cuda_stream)
+        _native.check(rc, "ldpc_mc_ml_batch_dev")
+    return run
+
+
 class _Ensemble:
     """Stand-in for a graph in ensemble mode (only n is needed by the counters)."""
 
@@ -55,10 +74,16 @@ class _Ensemble:
 
 
 class MonteCarlo:
-    """counters = [trials, frame_errors, bit_errors, iterations, curve[0..max_iters]] (int64)."""
+    """counters = [trials, frame_errors, bit_errors, iterations, curve[0..max_iters]] (int64).
+
+    optimal=True adds ML ("optimal") decoding of every trial's BEC word
+    (parallel_simulator.py `optimal`, modes 1/2/4/5): counters_ml = [trials,
+    ML frame errors, ML bit errors, 0, ML bit errors]; message_passing=False
+    drops the BP decode and the stop rule then counts ML frame errors."""
 
     def __init__(self, graph, channel, param, max_iters, algo="spa", alpha=1.0, early_stop=True,
-                 expurgation=-1, seed=0, batch=4096, process_group=None, executor=None, device=None):
+                 expurgation=-1, seed=0, batch=4096, process_group=None, executor=None, device=None,
+                 optimal=False, message_passing=True):
         import torch
         self.torch = torch
         self.graph = graph
@@ -80,9 +105,19 @@ class MonteCarlo:
             device = torch.device("cuda", torch.cuda.current_device()) if executor is None else torch.device("cpu")
         self.device = torch.device(device)
         self.counters = torch.zeros(_native.MC_NCOUNT + self.max_iters + 1, dtype=torch.int64, device=self.device)
+        self.optimal = bool(optimal)
+        self.message_passing = bool(message_passing) or not self.optimal
+        self.counters_ml = (torch.zeros(_native.MC_NCOUNT + 1, dtype=torch.int64, device=self.device)
+                            if self.optimal else None)
+        if self.optimal and self.channel != CHANNELS["bec"]:
+            raise ValueError("ML (optimal) decoding is defined for the BEC only")
         if executor is None:
-            executor = (ensemble_executor(self, graph.n, graph.dv, graph.dc) if isinstance(graph, _Ensemble)
-                        else device_executor(self))
+            if self.optimal:
+                executor = ml_executor(self)
+            elif isinstance(graph, _Ensemble):
+                executor = ensemble_executor(self, graph.n, graph.dv, graph.dc)
+            else:
+                executor = device_executor(self)
         self.executor = executor
         self.rounds = 0
 
@@ -99,6 +134,8 @@ class MonteCarlo:
 
     def _global(self):
         c = self.counters.clone()
+        if self.optimal:
+            c = self.torch.cat([c, self.counters_ml])
         if self.dist is not None and self.world > 1:
             if self.dist.get_backend(self.pg) == "gloo":
                 c = c.cpu()
@@ -116,9 +153,11 @@ class MonteCarlo:
             self.run_batch(first_cw, self.batch, stop)
             self.rounds += 1
             g = self._global()
-            if stop_frame_errors and g[1] >= stop_frame_errors:
+            frames = g[1] if self.message_passing else g[len(self.counters) + 1]
+            if stop_frame_errors and frames >= stop_frame_errors:
                 break
-            if num_tests and g[0] >= num_tests:
+            trials = g[0] if self.message_passing else g[len(self.counters)]
+            if num_tests and trials >= num_tests:
                 break
             if time_limit is not None and time.time() - t0 > time_limit:
                 break
@@ -127,9 +166,20 @@ class MonteCarlo:
     def results(self, g=None):
         g = self._global() if g is None else g
         n = self.graph.n
+        nc = len(self.counters)
+        out = {}
+        if self.optimal:
+            ml = g[nc:]
+            t = int(ml[0])
+            out = {"ml_num_tests": t, "ml_frame_errors": int(ml[1]), "ml_bit_errors": int(ml[2]),
+                   "ml_fer": ml[1] / t if t else float("nan"), "ml_ber": ml[2] / (t * n) if t else float("nan")}
+            g = g[:nc]
+            if not self.message_passing:
+                out.update({"num_tests": t, "raw_counters": g})
+                return out
         trials = int(g[0])
         curve = g[_native.MC_NCOUNT:].astype(np.float64)
-        return {
+        return {**out,
             "num_tests": trials,
             "frame_errors": int(g[1]),
             "bit_errors": int(g[2]),

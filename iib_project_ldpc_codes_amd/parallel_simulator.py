@@ -13,8 +13,9 @@ Same names, argument meaning and output format as the reference:
 Engines: ``engine="device"`` (default) runs the trial loop as fused device
 batches (montecarlo.MonteCarlo: Philox channel, exact sequential stop rule);
 ``engine="per_trial"`` keeps the reference's per-trial loop (numpy channel,
-one drop-in call per trial).  ML ("optimal") decoding is not provided
-(SURVEY.md 8f-3): modes 1, 2, 4, 5 raise NotImplementedError.
+one drop-in call per trial).  ML ("optimal") decoding (modes 1, 2, 4, 5) runs
+on the device too: ``optimal_decode`` calls ldpc_ml_decode_batch, the device
+engine ldpc_mc_ml_batch_dev.
 """
 import csv
 import ctypes as ct
@@ -75,8 +76,23 @@ class regular_LDPC_code:  # noqa: N801  (reference name)
         self.dc = dc
         self.rate = self.k / self.n
 
+    def _graph(self):
+        if getattr(self, "_tanner", None) is None:
+            self._tanner = TannerGraph.from_parity_check(np.asarray(self.parity_check))
+        return self._tanner
+
     def optimal_decode(self, binary_sequence):
-        raise NotImplementedError("ML (optimal) erasure decoding is out of scope (SURVEY.md 8f-3)")
+        """parallel_simulator.py:60-129 on libldpc_mi355x.so (ldpc_ml_decode_batch):
+        erasures (2) solved by GF(2) elimination, 2 left where the reference's loop
+        gives an unknown up; words with no erasure or more than n-k are returned as given."""
+        from .decoder import ml_decode
+        word = np.asarray(binary_sequence)
+        no_erasures = np.count_nonzero(word == 2)
+        if no_erasures == 0 or no_erasures > (self.n - self.k):
+            print("Either no erasures, or too many to be able to solve")
+            return binary_sequence
+        out, _ = ml_decode(self._graph(), word.astype(np.uint8)[None, :])
+        return out[0].astype(np.int64)
 
     def message_pass_decode(self, binary_sequence, max_its, check_lookup=None, variable_lookup=None):
         """parallel_simulator.py:131-166, backed by libldpc_mi355x.so:message_passing."""
@@ -165,36 +181,70 @@ def _device_ensemble_loop(parameter_set, expurgation, stop_frames, time_limit):
     return mc.results()
 
 
-def _per_trial_loop(LDPC_fn, parameter_set, expurgation, stop_frames, time_limit):
+def _per_trial_loop(LDPC_fn, parameter_set, expurgation, stop_frames, time_limit, optimal=False,
+                    message_passing=True):
     """The reference's own loop (parallel_simulator.py:198-244) with per-trial drop-in calls."""
     sim_BEC = BEC(parameter_set["BEC"])
     num_tests = parameter_set["num_tests"]
     iterations = parameter_set["iterations"]
     n = parameter_set["n"]
     curve = np.zeros(iterations + 1)
-    frames = bits = 0
+    frames = bits = ml_frames = ml_bits = 0
     i = 0
     start = datetime.now()
-    while frames < stop_frames and i < num_tests and (datetime.now() - start).total_seconds() < time_limit:
+    while ((frames if message_passing else ml_frames) < stop_frames and i < num_tests
+           and (datetime.now() - start).total_seconds() < time_limit):
         LDPC, check_lookup, variable_lookup = LDPC_fn(i)
         channel_output = sim_BEC.new_transmit(np.zeros(n))
-        _, errors = LDPC.message_pass_decode(channel_output, iterations, check_lookup, variable_lookup)
-        if errors[-1] > expurgation:
-            curve += errors
-            if errors[-1] != 0:
-                frames += 1
-            bits += errors[-1]
+        if message_passing:
+            _, errors = LDPC.message_pass_decode(channel_output, iterations, check_lookup, variable_lookup)
+            if errors[-1] > expurgation:
+                curve += errors
+                if errors[-1] != 0:
+                    frames += 1
+                bits += errors[-1]
+        if optimal:
+            decoded = LDPC.optimal_decode(channel_output)
+            count = int(np.count_nonzero(np.asarray(decoded) == 2))
+            ml_frames += count > 0
+            ml_bits += count
         i += 1
     return {"num_tests": i, "frame_errors": frames, "bit_errors": int(bits),
-            "error_curve": curve / (n * i) if i else curve}
+            "error_curve": curve / (n * i) if i else curve, "ml_frame_errors": int(ml_frames),
+            "ml_bit_errors": int(ml_bits)}
+
+
+def _device_ml_loop(graph, parameter_set, expurgation, stop_frames, time_limit):
+    """Optimal modes on the device: ML (+ message passing) per trial in fused batches."""
+    from .montecarlo import MonteCarlo
+    mp = bool(parameter_set.get("message_passing", True))
+    mc = MonteCarlo(graph, "bec", parameter_set["BEC"], parameter_set["iterations"], expurgation=expurgation,
+                    seed=int(parameter_set.get("seed", parameter_set.get("filenumber", 0))),
+                    batch=int(parameter_set.get("batch", DEFAULT_BATCH)), optimal=True, message_passing=mp)
+    t0 = datetime.now()
+    num_tests = parameter_set["num_tests"]
+    while True:
+        res = mc.results()
+        done = res["num_tests"]
+        B = min(mc.batch, num_tests - done)
+        if B <= 0:
+            break
+        mc.run_batch(done, B, stop_frames)
+        res = mc.results()
+        frames = res["frame_errors"] if mp else res["ml_frame_errors"]
+        if frames >= stop_frames or res["num_tests"] >= num_tests:
+            break
+        if time_limit and (datetime.now() - t0).total_seconds() >= time_limit:
+            break
+    return mc.results()
 
 
 def _run(parameter_set, fixed, expurgation=-1, prefix="regular_code", time_limit=43000.0):
     n, dv, dc = parameter_set["n"], parameter_set["dv"], parameter_set["dc"]
     iterations = parameter_set["iterations"]
     k = int(n * (dc - dv) / dc)
-    if parameter_set.get("optimal"):
-        raise NotImplementedError("ML (optimal) erasure decoding is out of scope (SURVEY.md 8f-3)")
+    optimal = bool(parameter_set.get("optimal"))
+    message_passing = bool(parameter_set.get("message_passing", True))
     engine = parameter_set.get("engine", "device")
     seed = int(parameter_set.get("seed", parameter_set.get("filenumber", 0)))
     if fixed:
@@ -202,21 +252,31 @@ def _run(parameter_set, fixed, expurgation=-1, prefix="regular_code", time_limit
         fn_graph = lambda i: code  # noqa: E731
     else:
         fn_graph = lambda i: TannerGraph.random_regular(n, dv, dc, seed=(seed, i))  # noqa: E731
-    if engine == "device" and not fixed:
+    if engine == "device" and optimal:
+        from .montecarlo import _Ensemble
+        res = _device_ml_loop(code if fixed else _Ensemble(n, dv, dc), parameter_set, expurgation, 200, time_limit)
+    elif engine == "device" and not fixed:
         res = _device_ensemble_loop(parameter_set, expurgation, 200, time_limit)
     elif engine == "device":
         res = _device_loop(fn_graph, parameter_set, expurgation, 200, time_limit)
     else:
         def ldpc_fn(i):
             g = fn_graph(i)
-            return (regular_LDPC_code(None, n, k, dv, dc), g.check_lookup, g.variable_lookup)
-        res = _per_trial_loop(ldpc_fn, parameter_set, expurgation, 200, time_limit)
+            return (regular_LDPC_code(g.parity_check(), n, k, dv, dc), g.check_lookup, g.variable_lookup)
+        res = _per_trial_loop(ldpc_fn, parameter_set, expurgation, 200, time_limit, optimal, message_passing)
     num_tests = res["num_tests"]
     fname = _filename(prefix, parameter_set, n, k, dv, dc, iterations, num_tests,
-                      code_number=parameter_set["filenumber"] if fixed else None)
+                      code_number=parameter_set["filenumber"] if fixed else None, message_passing=message_passing)
     if parameter_set.get("write_csv", True):
-        write_message_passing_file(fname, res["error_curve"], res["frame_errors"] / num_tests,
-                                   res["bit_errors"] / (num_tests * n))
+        if optimal and message_passing:
+            write_combined_file(fname, res["error_curve"], res["frame_errors"] / num_tests,
+                                res["bit_errors"] / (num_tests * n), res["ml_frame_errors"] / num_tests,
+                                res["ml_bit_errors"] / (num_tests * n))
+        elif optimal:
+            write_optimal_file(fname, res["ml_frame_errors"] / num_tests, res["ml_bit_errors"] / (num_tests * n))
+        else:
+            write_message_passing_file(fname, res["error_curve"], res["frame_errors"] / num_tests,
+                                       res["bit_errors"] / (num_tests * n))
     res["filename"] = fname
     return res
 

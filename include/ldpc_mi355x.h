@@ -180,6 +180,49 @@ int ldpc_mc_ensemble_batch_dev(int n, int dv, int dc, int channel, float param, 
                                int64_t stop_frame_errors, int64_t *d_counters, void *stream);
 
 /* ---------------------------------------------------------------------- */
+/* ML ("optimal") erasure decoding                        */
+/* ---------------------------------------------------------------------- */
+/*
+ * Replaces regular_LDPC_code.optimal_decode (parallel_simulator.py:60-129;
+ * expurgated :60-129) together with the ml_decode set-up it calls through ctypes
+ * (ml_decoder.c:7-36, bound at parallel_simulator.py:83-84) and the GF(2)
+ * row_reduce of the galois package (:89-91, :108).  Words are uint8 [B][n]:
+ * 0/1 known bits, 2 erasures (any other non-zero value is a known 1 and is
+ * returned as given).  Output: the decoded words, 2 where an unknown was given up
+ * by the reference's loop (first non-pivot column dropped with all its checks,
+ * system reduced again); words with no erasure or more erasures than n-k are
+ * returned unchanged.  unsolved int32 [B] = the number of 2s in each output word
+ * (the reference's optimal_error_count, :235).  d_out may alias d_words.
+ * Needs m = n-k <= 1000 (the range in which the reference's 1000-unknown cap,
+ * :96, never binds) and n <= 32767; otherwise LDPC_EINVAL.
+ */
+int ldpc_ml_decode_batch_dev(const ldpc_graph *g, const uint8_t *d_words, int B, uint8_t *d_out,
+                             int32_t *d_unsolved, void *stream);
+int ldpc_ml_decode_batch(const ldpc_graph *g, const uint8_t *words, int B, uint8_t *out, int32_t *unsolved);
+
+/* Ensemble form: word b is decoded on graph b of d_check_lookup int32[B][n*dv]
+ * (the ldpc_sample_regular_dev output layout). */
+int ldpc_ml_ensemble_decode_dev(int n, int dv, int dc, const int32_t *d_check_lookup, const uint8_t *d_words, int B,
+                                uint8_t *d_out, int32_t *d_unsolved, void *stream);
+
+/*
+ * Monte-Carlo batch of the "optimal" modes 1/2/4/5 (parallel_simulator.py:
+ * 168-272 / 274-401, `optimal` = True): BEC(eps) channel word t = first_cw + b,
+ * ML-decoded; with message_passing != 0 the same word is also BEC-decoded for
+ * max_iters iterations (modes 2/5).  g == NULL: ensemble mode, trial t decodes on
+ * graph t of the (n, dv, dc) sampler (ldpc_sample_regular law, key = seed);
+ * otherwise n/dv/dc are ignored.  d_counters_ml int64[LDPC_MC_NCOUNT + 1] =
+ * [trials, ML frame errors, ML bit errors (# of 2s), 0, # of 2s];
+ * d_counters_mp int64[LDPC_MC_NCOUNT + max_iters + 1] as ldpc_mc_batch_dev
+ * (expurgation applies to it only, as parallel_simulator_expurgated.py:238-245).
+ * The sequential stop rule counts message-passing frame errors when
+ * message_passing != 0, ML frame errors otherwise (parallel_simulator.py:186-242).
+ */
+int ldpc_mc_ml_batch_dev(const ldpc_graph *g, int n, int dv, int dc, float eps, uint64_t seed, uint64_t first_cw,
+                         int B, int max_iters, int message_passing, int expurgation, int64_t stop_frame_errors,
+                         int64_t *d_counters_mp, int64_t *d_counters_ml, void *stream);
+
+/* ---------------------------------------------------------------------- */
 /* Diagnostics (host only, no GPU needed)                                  */
 /* ---------------------------------------------------------------------- */
 /*

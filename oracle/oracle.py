@@ -46,6 +46,12 @@ def lib():
         _lib.oracle_density_evolution.restype = i
         _lib.oracle_sample_regular.argtypes = [i, i, i, u64, u64, i, P, P]
         _lib.oracle_sample_regular.restype = i
+        _lib.oracle_ml_system.argtypes = [i, i, P, P, P, P, P]
+        _lib.oracle_ml_system.restype = None
+        _lib.oracle_ml_decode.argtypes = [i, i, P, P, P, P]
+        _lib.oracle_ml_decode.restype = i
+        _lib.oracle_ml_decode_batch.argtypes = [i, i, P, P, P, i, P, P]
+        _lib.oracle_ml_decode_batch.restype = None
         _lib.oracle_num_threads.argtypes = []
         _lib.oracle_num_threads.restype = i
     return _lib
@@ -152,6 +158,33 @@ def density_evolution(eps, iterations, dv, dc, threshold=0.0):
     return out[:ln]
 
 
+def ml_system(cptr, cvar, word, n, m):
+    """ml_decoder.c:7-36 restated: (target[m], remaining[ne, m]) as uint8."""
+    cptr = np.ascontiguousarray(cptr, np.int32)
+    cvar = np.ascontiguousarray(cvar, np.int32)
+    w = np.ascontiguousarray(word, np.uint8)
+    ne = int((w == 2).sum())
+    target = np.zeros(m, np.uint8)
+    rem = np.zeros(max(ne, 1) * m, np.uint8)
+    lib().oracle_ml_system(n, m, _p(cptr), _p(cvar), _p(w), _p(target), _p(rem))
+    return target, rem[: ne * m].reshape(ne, m)
+
+
+def ml_decode_batch(cptr, cvar, words, n, m):
+    """optimal_decode (parallel_simulator.py:60-129) restated, per word.
+    Returns (out_words uint8 [B, n] with 2 = unsolvable, unsolved int32 [B])."""
+    cptr = np.ascontiguousarray(cptr, np.int32)
+    cvar = np.ascontiguousarray(cvar, np.int32)
+    w = np.ascontiguousarray(words, np.uint8)
+    if w.ndim == 1:
+        w = w[None, :]
+    B = w.shape[0]
+    out = np.zeros((B, n), np.uint8)
+    uns = np.zeros(B, np.int32)
+    lib().oracle_ml_decode_batch(n, m, _p(cptr), _p(cvar), _p(w), B, _p(out), _p(uns))
+    return out, uns
+
+
 # --------------------------------------------------------------------------
 # Reference C (compiled from /root/reference by `make -C oracle ref`)
 # --------------------------------------------------------------------------
@@ -175,6 +208,22 @@ def ref_message_pass_decode(binary_sequence, max_its, check_lookup, variable_loo
                               errors.ctypes.data_as(ct.POINTER(ct.c_int)),
                               ct.c_int(n), ct.c_int(k), ct.c_int(dv), ct.c_int(dc))
     return seq, np.insert(errors, 0, initial), it
+
+
+def ref_ml_system(parity_check, word, n, dv, dc):
+    """Drive _ref/ml_decoder.so as parallel_simulator.py:72-88 does.
+    Returns (target[m] uint8, remaining[ne, m] uint8) before the transpose."""
+    k = int(n * (dc - dv) / dc)
+    ne = int(np.count_nonzero(np.asarray(word) == 2))
+    seq = np.array(word, dtype="int32")
+    target = np.zeros(n - k, dtype="bool")
+    rem = np.zeros(max(ne, 1) * (n - k), dtype="bool")
+    H = np.ascontiguousarray(parity_check, dtype="bool")
+    lib_ = ct.CDLL(os.path.join(REF_DIR, "ml_decoder.so"))
+    lib_.ml_decode(seq.ctypes.data_as(ct.POINTER(ct.c_int)), target.ctypes.data_as(ct.POINTER(ct.c_bool)),
+                   H.ctypes.data_as(ct.POINTER(ct.c_bool)), rem.ctypes.data_as(ct.POINTER(ct.c_bool)),
+                   ct.c_int(n), ct.c_int(dv), ct.c_int(dc))
+    return target.astype(np.uint8), rem[: ne * (n - k)].astype(np.uint8).reshape(ne, n - k)
 
 
 def ref_generate_random_code(n, dv, dc):

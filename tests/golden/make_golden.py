@@ -13,6 +13,11 @@ Outputs (committed; data only -- inputs and the reference's outputs):
                    with the initial erasure count prepended, return index).
                    Raw-C cases with caller-populated errors[] pin the `+=`
                    accumulation of message_passing.c:73.
+  ml_golden.npz    ML-decoder system set-up: graphs (and dense H) drawn by the
+                   reference's random_code_generator.c, channel words, and the
+                   (target, remaining_parity_checks) buffers the reference's
+                   ml_decoder.c fills, driven as parallel_simulator.py:72-88.
+                   (`python tests/golden/make_golden.py ml` regenerates only this.)
   de_golden.json   BEC density evolution / threshold known answers computed by
                    the reference's tools/density_evolution.py:9-16 and
                    test_de_threshold.py:17-28, finite_length_scaling_calculation.py.
@@ -124,6 +129,37 @@ def de_cases():
     print("de_golden.json:", {k: (v if not isinstance(v, list) else len(v)) for k, v in res.items()})
 
 
+def ml_cases():
+    assert oracle.ref_available(), "run `make -C oracle ref` first"
+    rs = np.random.RandomState(20261016)
+    out = {}
+    cases = 0
+    for gi, (n, dv, dc) in enumerate([(12, 3, 6), (60, 3, 6), (100, 3, 6), (64, 4, 8)]):
+        chk, var, H = oracle.ref_generate_random_code(n, dv, dc)
+        out[f"g{gi}_n"] = np.array([n, dv, dc], np.int32)
+        out[f"g{gi}_c2v"] = np.asarray(chk, np.int32)
+        out[f"g{gi}_H"] = np.asarray(H, np.uint8)
+        for eps in (0.1, 0.3, 0.4, 0.45, 0.5):
+            for _ in range(3):
+                word = np.where(rs.rand(n) < eps, 2, 0)
+                if cases % 2:  # non-codeword known values too
+                    word = np.where(word == 2, 2, rs.randint(0, 2, size=n))
+                target, rem = oracle.ref_ml_system(H, word, n, dv, dc)
+                out[f"c{cases}_meta"] = np.array([gi], np.int32)
+                out[f"c{cases}_word"] = word.astype(np.uint8)
+                out[f"c{cases}_target"] = target
+                out[f"c{cases}_remaining"] = rem
+                cases += 1
+    out["num_cases"] = np.array([cases], np.int32)
+    out["num_graphs"] = np.array([4], np.int32)
+    np.savez_compressed(os.path.join(HERE, "ml_golden.npz"), **out)
+    print(f"ml_golden.npz: {cases} cases")
+
+
 if __name__ == "__main__":
-    reference_cases()
-    de_cases()
+    if sys.argv[1:] == ["ml"]:
+        ml_cases()
+    else:
+        reference_cases()
+        ml_cases()
+        de_cases()

@@ -192,6 +192,51 @@ def test_minsum_bit_exact(torch, irregular, early_stop):
     np.testing.assert_array_equal(its, oits)
 
 
+@pytest.mark.parametrize("irregular", [False, True])
+def test_early_stop_stops_only_on_codewords(torch, irregular):
+    """Syndrome early stop: a frame that stops before max_iters must carry a valid
+    codeword (for the regular distinct-column code the all-zero one; the irregular
+    code has low-weight codewords a decoder can converge to).  Large batches at the
+    headline shape (LDS-resident kernel) and on an irregular graph (generic kernel);
+    this catches a hard-decision write racing with the syndrome read."""
+    from iib_project_ldpc_codes_amd import decoder, ensembles
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = (ensembles.sample_irregular(ensembles.RSU_DL4, 4000, seed=2, deg2="zigzag") if irregular
+         else TannerGraph.random_regular(10000, 3, 6, seed=1, distinct_columns=True))
+    for algo, ch, p in (("minsum", "bsc", 0.05), ("spa", "awgn", 0.80)):
+        llr = decoder.channel_dev(ch, p, 11, 0, g.n, 65536)
+        _, hard, its = decoder.bp_decode_dev(g, llr, 50, algo, alpha=0.75 if algo == "minsum" else 1.0,
+                                             early_stop=True, want_post=False)
+        torch.cuda.synchronize()
+        stopped = its < 50
+        assert int(stopped.sum()) > 60000
+        # syndrome of every stopped frame's decision (slot -> check via cptr)
+        cptr, cvar, _, _ = g.to_csr()
+        slot_check = torch.from_numpy(np.repeat(np.arange(g.m), np.diff(cptr))).cuda()
+        bits = hard[stopped][:, torch.from_numpy(cvar.astype(np.int64)).cuda()].to(torch.int32)
+        par = torch.zeros((bits.shape[0], g.m), dtype=torch.int32, device="cuda")
+        par.index_add_(1, slot_check, bits)
+        assert int((par % 2).sum()) == 0, algo
+        if not irregular:  # no low-weight codewords here: stopped frames are error-free
+            assert int(hard[stopped].sum()) == 0, algo
+
+
+def test_minsum_early_stop_headline_bit_exact(torch):
+    """Min-sum with early stop at n = 10000, 4096 frames: decisions and stop iterations
+    identical to the oracle on every frame."""
+    from iib_project_ldpc_codes_amd import decoder
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = TannerGraph.random_regular(10000, 3, 6, seed=1, distinct_columns=True)
+    csr = g.to_csr()
+    llr = decoder.channel_dev("bsc", 0.06, 12, 0, g.n, 4096)
+    post, hard, its = decoder.bp_decode_dev(g, llr, 50, "minsum", alpha=0.75, early_stop=True)
+    torch.cuda.synchronize()
+    opost, ohard, oits = oracle.bp_decode_batch(csr, llr.cpu().numpy(), 50, 1, alpha=0.75, early_stop=True)
+    np.testing.assert_array_equal(its.cpu().numpy(), oits)
+    np.testing.assert_array_equal(hard.cpu().numpy(), ohard)
+    np.testing.assert_array_equal(post.cpu().numpy(), opost)
+
+
 def test_spa_early_stop_iterations(torch):
     from iib_project_ldpc_codes_amd import decoder
     g, csr, llr = _soft_case(1000, 128, 0.70, 14)
