@@ -79,8 +79,13 @@ hipError_t launch_mc_reduce(const int32_t *trial, const int32_t *trial_its, int 
                             int expurgation, int64_t stop_frame_errors, int64_t *d_counters,
                             int32_t *d_cutoff, hipStream_t stream);
 
+// Buckets (= threads per workgroup) of the parallel graph sampler for n*dv
+// sockets; the permutation is in LDS (u16) when n*dv < 65536.  Must match
+// oracle_sample_regular.
+inline int sample_buckets(int E) { return E <= 16384 ? 256 : (E < 65536 ? 512 : 1024); }
+
 // Random regular graphs on the device (law of random_code_generator.c), one
-// thread per graph; attempts[g] = number of permutations drawn (negative if
+// workgroup per graph; attempts[g] = number of permutations drawn (negative if
 // max_attempts was hit without a valid graph).
 hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
                                  int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts,

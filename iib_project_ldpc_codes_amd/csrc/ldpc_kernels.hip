@@ -28,6 +28,12 @@ constexpr int kWave = 64;
 #ifndef LDPC_ABLATE_VARW
 #define LDPC_ABLATE_VARW 0
 #endif
+#ifndef LDPC_SAMPLER_FIXED_ATT
+#define LDPC_SAMPLER_FIXED_ATT 0  // timing ablation only: exactly this many permutations per graph
+#endif
+#ifndef LDPC_SAMPLER_SKIP
+#define LDPC_SAMPLER_SKIP 0       // timing ablation only: 2 = no Fisher-Yates, 8 = no variable_lookup
+#endif
 #ifndef LDPC_CHECK_UNROLL
 #define LDPC_CHECK_UNROLL 1
 #endif
@@ -85,6 +91,29 @@ __device__ __forceinline__ uint8_t chan_bec(const ChanArgs &ch, uint64_t cw, int
 // ---------------------------------------------------------------------------
 // Block reductions (wave64)
 // ---------------------------------------------------------------------------
+// Exclusive prefix sum over the workgroup (any multiple of 64 threads <= 1024);
+// `total` gets the sum.  Contains two barriers.
+__device__ __forceinline__ int block_excl_scan(int x, int *wsum, int &total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int incl = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, kWave);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int w = 0; w < nw; ++w) {
+        const int v = wsum[w];
+        base += (w < wave) ? v : 0;
+        tot += v;
+    }
+    __syncthreads();
+    total = tot;
+    return base + incl - x;
+}
+
 __device__ __forceinline__ int wave_sum(int x) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
@@ -625,29 +654,39 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
 //
 // Configuration model: a uniform permutation of the n*dv sockets, check c =
 // positions [c*dc, c*dc+dc), variable of a socket = socket / dv, and a whole-
-// graph redraw whenever a check holds a variable twice (:39-47).  One thread per
-// graph runs Fisher-Yates from the end, so check c is complete as soon as
-// position c*dc is fixed and a bad check aborts the attempt at once -- the same
-// conditional law as drawing the whole permutation and rejecting it (the next
-// attempt reshuffles the current array, as the reference's recursion does).
-// Draw k of graph g is word k%4 of Philox(ctr = {k/4, 'GRPH', g_lo, g_hi},
-// key = seed); j = uniform on [0, i] by Lemire's multiply with rejection
-// (the reference's rand() % (i+1) carries a small modulo bias we do not copy).
+// graph redraw whenever a check holds a variable twice (:39-47) -- i.e. a
+// uniformly random permutation conditioned on every check being simple.  For
+// (3, 6) that condition holds with probability ~0.0074, so a graph costs ~135
+// permutations; they are drawn in parallel by one workgroup per graph with the
+// Rao-Sandelius method, which is exactly uniform:
+//   1. every socket s draws a bucket in [0, K) (K = workgroup size, the top
+//      log2 K bits of word (s>>6)&3 of Philox ctr {(s>>8)<<6 | s&63,
+//      tag|att<<2|0, g_lo, g_hi}, key = seed); a stable counting sort (bucket-major, socket order within a
+//      bucket) lays the buckets out back to back -- per-wave ranks come from
+//      log2 K ballots, offsets from a workgroup scan;
+//   2. thread t Fisher-Yates-shuffles bucket t from its end, drawing j uniform on
+//      [0, i] by Lemire's multiply-with-rejection from its own Philox stream
+//      ctr {t<<20 | block, tag|att<<2|1, g_lo, g_hi};
+//   3. every check is tested for a repeated variable; any failure redraws the
+//      whole permutation (att + 1).
+// Variable ids (socket / dv) are permuted instead of sockets: every output
+// depends on a socket only through its variable.  The permutation lives in LDS
+// (u16) when n*dv < 65536, else in the caller's check_lookup row.
 // Output: check_lookup[g][E] (variable ids, check-major) and variable_lookup
 // [g][E] (each variable's checks ascending), the reference's edge-list format.
 // oracle_sample_regular restates this bit for bit.
 // ===========================================================================
-constexpr uint32_t kGraphTag = 0x48505247u;  // 'GRPH'
+constexpr uint32_t kSampleTag = 0x80000000u;  // never 0: channel draws use ctr[1] = 0
 
-struct GraphRng {
-    uint32_t k0, k1, g0, g1;
-    uint64_t k = 0;
+struct BucketRng {  // sequential Philox stream of one bucket
+    uint32_t k0, k1, c0, c1, g0, g1;
+    uint32_t k = 0;
     uint4 blk;
     __device__ __forceinline__ uint32_t next() {
-        const uint32_t w = (uint32_t)(k & 3);
-        if (w == 0) blk = philox_block((uint32_t)(k >> 2), kGraphTag, g0, g1, k0, k1);
+        const uint32_t w = k & 3;
+        if (w == 0) blk = philox_block(c0 | (k >> 2), c1, g0, g1, k0, k1);
         ++k;
-        return pick4(blk, w);
+        return pick4(blk, (int)w);
     }
     __device__ __forceinline__ uint32_t below(uint32_t range) {  // uniform on [0, range)
         uint64_t m = (uint64_t)next() * range;
@@ -663,127 +702,145 @@ struct GraphRng {
     }
 };
 
-// Both kernels permute variable ids (socket / dv) rather than sockets: the
-// draws are identical and every output depends on the socket only through its
-// variable, so the graphs are the same -- without integer divisions on the
-// dependent swap chain.  Position bookkeeping uses countdowns, not modulo.
-template <typename Idx, typename Acc>
-__device__ __forceinline__ bool sample_one(int E, int dc, GraphRng &rng, Acc S, int max_attempts, int &att) {
-    bool ok = false;
-    att = 0;
-    auto check_ok = [&](int first) {
-        for (int x = first; x < first + dc; ++x) {
-            const Idx vx = S(x);
-            for (int y = x + 1; y < first + dc; ++y)
-                if (S(y) == vx) return false;
-        }
-        return true;
-    };
-    while (!ok && att < max_attempts) {
-        ++att;
-        ok = true;
-        int to_check = (E - 1) % dc;  // steps until position i is a multiple of dc
-        for (int i = E - 1; i >= 1; --i) {
-            const int j = (int)rng.below((uint32_t)i + 1u);
-            const Idx t = S(i);
-            S(i) = S(j);
-            S(j) = t;
-            if (to_check == 0) {
-                to_check = dc;
-                if (!check_ok(i)) { ok = false; break; }
-            }
-            --to_check;
-        }
-        if (ok && !check_ok(0)) ok = false;
-    }
-    return ok;
-}
-
-__global__ __launch_bounds__(64) void sample_regular_kernel(int n, int dv, int dc, uint32_t k0, uint32_t k1,
-                                                            uint64_t first_graph, int G, int32_t *check_lookup,
-                                                            int32_t *variable_lookup, int32_t *attempts,
-                                                            int max_attempts) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= G) return;
-    const int E = n * dv;
-    int32_t *seq = check_lookup + (size_t)g * E;  // permuted variable ids == check_lookup
-    int32_t *vl = variable_lookup + (size_t)g * E;
-    const uint64_t gid = first_graph + (uint64_t)g;
-    GraphRng rng{k0, k1, (uint32_t)gid, (uint32_t)(gid >> 32)};
-    for (int v = 0, s = 0; v < n; ++v)
-        for (int t = 0; t < dv; ++t) seq[s++] = v;
-    int att = 0;
-    const bool ok = sample_one<int32_t>(E, dc, rng, [&](int x) -> int32_t & { return seq[x]; }, max_attempts, att);
-    if (attempts) attempts[g] = ok ? att : -att;
-    // variable_lookup: scanning positions in order fills each row in ascending check order
-    for (int v = 0; v < n; ++v)
-        for (int t = 0; t < dv; ++t) vl[(size_t)v * dv + t] = -1;
-    for (int s = 0, c = 0, r = 0; s < E; ++s) {
-        int32_t *row = vl + (size_t)seq[s] * dv;
-        int k = 0;
-        while (row[k] >= 0) ++k;
-        row[k] = c;
-        if (++r == dc) { r = 0; ++c; }
-    }
-}
-
-// LDS-resident form for n*dv < 65536: each lane of a 64-thread workgroup owns
-// one graph whose permutation lives in LDS as u16 (lane-interleaved); the
-// whole wave then writes the graphs out.  Same draws, same output.
-__global__ __launch_bounds__(64) void sample_regular_lds_kernel(int n, int dv, int dc, uint32_t k0, uint32_t k1,
-                                                                uint64_t first_graph, int G, int per_wg,
-                                                                int32_t *check_lookup, int32_t *variable_lookup,
-                                                                int32_t *attempts, int max_attempts) {
+template <int T, typename Idx, bool LDSBUF>
+__global__ __launch_bounds__(T) void sample_regular_kernel(int n, int dv, int dc, uint32_t k0, uint32_t k1,
+                                                           uint64_t first_graph, int32_t *check_lookup,
+                                                           int32_t *variable_lookup, int32_t *attempts,
+                                                           int max_attempts) {
+    constexpr int NW = T / kWave;
+    constexpr int LOGK = T == 256 ? 8 : (T == 512 ? 9 : 10);
     extern __shared__ __align__(16) unsigned char smem[];
-    const int E = n * dv;
-    const int lane = threadIdx.x;
-    const int g0 = blockIdx.x * per_wg;
-    const int ng = min(per_wg, G - g0);
-    uint16_t *seqs = reinterpret_cast<uint16_t *>(smem);  // element x of local graph l at x*per_wg + l
-    for (int x = lane; x < E * per_wg; x += 64) seqs[x] = (uint16_t)((x / per_wg) / dv);
-    __syncthreads();
-    if (lane < ng) {
-        const int l = lane;
-        const uint64_t gid = first_graph + (uint64_t)(g0 + l);
-        GraphRng rng{k0, k1, (uint32_t)gid, (uint32_t)(gid >> 32)};
-        int att = 0;
-        const bool ok = sample_one<uint16_t>(
-            E, dc, rng, [&](int x) -> uint16_t & { return seqs[x * per_wg + l]; }, max_attempts, att);
-        if (attempts) attempts[g0 + l] = ok ? att : -att;
-    }
-    __syncthreads();
-    for (int l = 0; l < ng; ++l) {  // the wave writes graph l out
-        int32_t *chk = check_lookup + (size_t)(g0 + l) * E;
-        for (int x = lane; x < E; x += 64) chk[x] = seqs[x * per_wg + l];
-    }
-    // variable_lookup: claim a row slot per position (atomic CAS on -1), then sort rows
-    for (int l = 0; l < ng; ++l) {
-        int32_t *vl = variable_lookup + (size_t)(g0 + l) * E;
-        for (int x = lane; x < E; x += 64) vl[x] = -1;
-    }
-    __threadfence_block();
-    __syncthreads();
-    for (int l = 0; l < ng; ++l) {
-        int32_t *vl = variable_lookup + (size_t)(g0 + l) * E;
-        for (int x = lane; x < E; x += 64) {
-            int32_t *row = vl + (size_t)seqs[x * per_wg + l] * dv;
-            const int c = x / dc;
-            for (int k = 0; k < dv; ++k)
-                if (atomicCAS(&row[k], -1, c) == -1) break;
+    int *cnt = reinterpret_cast<int *>(smem);  // [T buckets][NW waves]
+    int *wsum = cnt + T * NW;                  // [16]
+    const int E = n * dv, m = E / dc;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t gid = first_graph + blockIdx.x;
+    const uint32_t g0 = (uint32_t)gid, g1 = (uint32_t)(gid >> 32);
+    int32_t *chk = check_lookup + (size_t)blockIdx.x * E;
+    Idx *buf = LDSBUF ? reinterpret_cast<Idx *>(wsum + 16) : reinterpret_cast<Idx *>(chk);
+    const int chunk = ((E + NW - 1) / NW + 255) / 256 * 256;
+    const int s_lo = min(E, wave * chunk), s_hi = min(E, s_lo + chunk);
+    const uint64_t lt_mask = (1ull << lane) - 1;
+
+    // bucket of socket s = base + lane (base a multiple of 64) from word (s>>6)&3 of
+    // the Philox block {(s>>8)<<6 | lane, c1, g}: one block per lane per 256 sockets;
+    // peers = the lanes of this 64-socket group in the same bucket
+    auto group = [&](int base, const uint4 &r, uint32_t &bk, uint64_t &peers) {
+        const int s = base + lane;
+        const bool valid = s < s_hi;
+        bk = valid ? pick4(r, (base >> 6) & 3) >> (32 - LOGK) : 0u;
+        peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < LOGK; ++bit) {
+            const bool on = (bk >> bit) & 1u;
+            const uint64_t bal = __ballot(valid && on);
+            peers &= on ? bal : ~bal;
         }
+        return valid;
+    };
+
+    int att = 0;
+    bool ok = false;
+    while (!ok && att < max_attempts) {
+        const uint32_t c1 = kSampleTag | ((uint32_t)att << 2);
+        for (int i = tid; i < T * NW; i += T) cnt[i] = 0;
+        __syncthreads();
+        // 1a. bucket sizes per (bucket, wave)
+        for (int b256 = s_lo; b256 < s_hi; b256 += 256) {
+            const uint4 r = philox_block((uint32_t)(((b256 >> 8) << 6) | lane), c1, g0, g1, k0, k1);
+            for (int base = b256; base < min(s_hi, b256 + 256); base += 64) {
+                uint32_t bk;
+                uint64_t peers;
+                if (group(base, r, bk, peers) && (peers & lt_mask) == 0) cnt[bk * NW + wave] += __popcll(peers);
+            }
+        }
+        __syncthreads();
+        // 1b. offsets: bucket-major, wave-minor (= socket order inside a bucket)
+        int size = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) size += cnt[tid * NW + w];
+        int total = 0;
+        const int start = block_excl_scan(size, wsum, total);
+        {
+            int run = start;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                const int c = cnt[tid * NW + w];
+                cnt[tid * NW + w] = run;
+                run += c;
+            }
+        }
+        __syncthreads();
+        // 1c. stable scatter of the variable ids
+        for (int b256 = s_lo; b256 < s_hi; b256 += 256) {
+            const uint4 r = philox_block((uint32_t)(((b256 >> 8) << 6) | lane), c1, g0, g1, k0, k1);
+            for (int base = b256; base < min(s_hi, b256 + 256); base += 64) {
+                uint32_t bk;
+                uint64_t peers;
+                if (group(base, r, bk, peers)) {
+                    const int s = base + lane;
+                    const int dst = cnt[bk * NW + wave] + __popcll(peers & lt_mask);
+                    buf[dst] = (Idx)(s / dv);
+                    if ((peers & lt_mask) == 0) cnt[bk * NW + wave] += __popcll(peers);
+                }
+            }
+        }
+        __syncthreads();
+        // 2. Fisher-Yates inside bucket `tid`
+        if (!(LDPC_SAMPLER_SKIP & 2)) {
+            BucketRng rng{k0, k1, (uint32_t)tid << 20, c1 | 1u, g0, g1};
+            Idx *bb = buf + start;
+            for (int i = size - 1; i >= 1; --i) {
+                const int j = (int)rng.below((uint32_t)i + 1u);
+                const Idx t = bb[i];
+                bb[i] = bb[j];
+                bb[j] = t;
+            }
+        }
+        __syncthreads();
+        // 3. every check simple?
+        int bad = 0;
+        for (int c = tid; c < m; c += T) {
+            const Idx *r = buf + (size_t)c * dc;
+            for (int x = 0; x < dc && !bad; ++x)
+                for (int y = x + 1; y < dc; ++y) bad |= (r[x] == r[y]);
+        }
+        ok = !__syncthreads_or(bad);
+        ++att;
+        if (LDPC_SAMPLER_FIXED_ATT > 0) ok = att >= LDPC_SAMPLER_FIXED_ATT;
+    }
+    if (attempts && tid == 0) attempts[blockIdx.x] = ok ? att : -att;
+    // check_lookup (variable ids per slot); variable_lookup rows claimed by CAS, then sorted
+    int32_t *vl = variable_lookup + (size_t)blockIdx.x * E;
+    if (LDPC_SAMPLER_SKIP & 8) {
+        if (LDPC_SAMPLER_FIXED_ATT > 0)
+            for (int x = tid; x < E; x += T) chk[x] = buf[x];
+        return;
+    }
+    for (int x = tid; x < E; x += T) {
+        if (LDSBUF) chk[x] = buf[x];
+        vl[x] = -1;
     }
     __threadfence_block();
     __syncthreads();
-    for (int l = 0; l < ng; ++l) {
-        int32_t *vl = variable_lookup + (size_t)(g0 + l) * E;
-        for (int v = lane; v < n; v += 64) {
-            int32_t *r = vl + (size_t)v * dv;
-            for (int x = 1; x < dv; ++x) {
-                const int key = r[x];
-                int y = x - 1;
-                while (y >= 0 && r[y] > key) { r[y + 1] = r[y]; --y; }
-                r[y + 1] = key;
+    for (int x = tid; x < E; x += T) {
+        int32_t *row = vl + (size_t)buf[x] * dv;
+        const int c = x / dc;
+        for (int k = 0; k < dv; ++k)
+            if (atomicCAS(&row[k], -1, c) == -1) break;
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int v = tid; v < n; v += T) {
+        int32_t *r = vl + (size_t)v * dv;
+        for (int x = 1; x < dv; ++x) {
+            const int key = r[x];
+            int y = x - 1;
+            while (y >= 0 && r[y] > key) {
+                r[y + 1] = r[y];
+                --y;
             }
+            r[y + 1] = key;
         }
     }
 }
@@ -956,27 +1013,6 @@ __global__ __launch_bounds__(256) void mc_reduce_kernel(const int32_t *trial, co
 // state[n] (u8: 0/1 known, 2 unknown, 3 given up, 4/5 solved 0/1);
 // rowchk[m], colvar[m] (int16); achk[m] (u8).
 
-__device__ __forceinline__ int ml_block_scan(int x, int *wsum, int &total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    int incl = x;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off, kWave);
-        if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    int base = 0, tot = 0;
-    for (int w = 0; w < nw; ++w) {
-        const int v = wsum[w];
-        base += (w < wave) ? v : 0;
-        tot += v;
-    }
-    __syncthreads();
-    total = tot;
-    return base + incl - x;
-}
-
 // Register-array helpers with static indices only (a data-dependent index would
 // push R[] to scratch): set bit k by masks, and drop the front word (the
 // elimination window: columns left of the current 64-column block are never read
@@ -1030,7 +1066,7 @@ __global__ __launch_bounds__(1024) void ml_kernel(const int32_t *__restrict__ cp
     for (int c = tid; c < m; c += T) achk[c] = 1;
     if (tid < 2) best[tid] = INT_MAX;
     int ne = 0;
-    (void)ml_block_scan(ne_local, wsum, ne);  // (its barriers also publish state / achk / best)
+    (void)block_excl_scan(ne_local, wsum, ne);  // (its barriers also publish state / achk / best)
     if (ne == 0 || ne > m) {
         for (int v = tid; v < n; v += T) w_out[v] = w_in[v];
         if (tid == 0) unsolved[b] = ne;
@@ -1044,7 +1080,7 @@ __global__ __launch_bounds__(1024) void ml_kernel(const int32_t *__restrict__ cp
         int cnt = 0;
         for (int v = v0; v < v1; ++v) cnt += (state[v] == 2);
         int ncols = 0;
-        int col = ml_block_scan(cnt, wsum, ncols);
+        int col = block_excl_scan(cnt, wsum, ncols);
         for (int v = v0; v < v1; ++v) {
             const int st = state[v];
             if (st == 2) {
@@ -1059,7 +1095,7 @@ __global__ __launch_bounds__(1024) void ml_kernel(const int32_t *__restrict__ cp
         cnt = 0;
         for (int c = c0; c < c1; ++c) cnt += achk[c];
         int nrows = 0;
-        int pos = ml_block_scan(cnt, wsum, nrows);  // barrier: code[] / colvar[] complete
+        int pos = block_excl_scan(cnt, wsum, nrows);  // barrier: code[] / colvar[] complete
         for (int c = c0; c < c1; ++c)
             if (achk[c]) rowchk[pos++] = (int16_t)c;
         __syncthreads();
@@ -1420,20 +1456,23 @@ hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t 
                                  int max_attempts, hipStream_t stream) {
     if (G <= 0) return hipSuccess;
     const int E = n * dv;
-    if (E < 65536) {
-        // graphs per workgroup: keep each workgroup's LDS <= 40 KiB (4 workgroups / CU)
-        int per = (int)std::min<long>(64, std::max<long>(1, 40960 / (2L * E)));
-        const size_t lds = (size_t)2 * E * per;
-        hipError_t e = allow_lds(sample_regular_lds_kernel, lds);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(sample_regular_lds_kernel, dim3((G + per - 1) / per), dim3(64), lds, stream, n, dv, dc,
-                           (uint32_t)seed, (uint32_t)(seed >> 32), first_graph, G, per, check_lookup, variable_lookup,
-                           attempts, max_attempts);
-        return hipGetLastError();
-    }
-    hipLaunchKernelGGL(sample_regular_kernel, dim3((G + 63) / 64), dim3(64), 0, stream, n, dv, dc, (uint32_t)seed,
-                       (uint32_t)(seed >> 32), first_graph, G, check_lookup, variable_lookup, attempts, max_attempts);
-    return hipGetLastError();
+    const int K = sample_buckets(E);
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const size_t ctl = (size_t)4 * (K * (K / kWave) + 16);
+#define LDPC_SAMPLE(TT, IDX, LDSB)                                                                             \
+    do {                                                                                                       \
+        auto k = sample_regular_kernel<TT, IDX, LDSB>;                                                         \
+        const size_t lds = ctl + (LDSB ? (size_t)2 * E : 0);                                                   \
+        hipError_t e = allow_lds(k, lds);                                                                      \
+        if (e != hipSuccess) return e;                                                                         \
+        hipLaunchKernelGGL(k, dim3(G), dim3(TT), lds, stream, n, dv, dc, k0, k1, first_graph, check_lookup,    \
+                           variable_lookup, attempts, max_attempts);                                           \
+        return hipGetLastError();                                                                              \
+    } while (0)
+    if (K == 256) LDPC_SAMPLE(256, uint16_t, true);
+    if (K == 512) LDPC_SAMPLE(512, uint16_t, true);
+    LDPC_SAMPLE(1024, int32_t, false);
+#undef LDPC_SAMPLE
 }
 
 hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,

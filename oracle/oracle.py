@@ -52,6 +52,8 @@ def lib():
         _lib.oracle_ml_decode.restype = i
         _lib.oracle_ml_decode_batch.argtypes = [i, i, P, P, P, i, P, P]
         _lib.oracle_ml_decode_batch.restype = None
+        _lib.oracle_sample_regular_batch.argtypes = [i, i, i, u64, u64, i, i, P, P, P]
+        _lib.oracle_sample_regular_batch.restype = None
         _lib.oracle_num_threads.argtypes = []
         _lib.oracle_num_threads.restype = i
     return _lib
@@ -149,6 +151,16 @@ def sample_regular(n, dv, dc, seed, graph, max_attempts=1 << 20):
     chk = np.zeros(n * dv, np.int32)
     var = np.zeros(n * dv, np.int32)
     att = lib().oracle_sample_regular(n, dv, dc, seed, graph, max_attempts, _p(chk), _p(var))
+    return chk, var, att
+
+
+def sample_regular_batch(n, dv, dc, seed, first_graph, G, max_attempts=1 << 20):
+    """G graphs first_graph.. of the device sampler's restatement (OpenMP).
+    Returns (check_lookup [G, n*dv], variable_lookup [G, n*dv], attempts [G])."""
+    chk = np.zeros((G, n * dv), np.int32)
+    var = np.zeros((G, n * dv), np.int32)
+    att = np.zeros(G, np.int32)
+    lib().oracle_sample_regular_batch(n, dv, dc, seed, first_graph, G, max_attempts, _p(chk), _p(var), _p(att))
     return chk, var, att
 
 

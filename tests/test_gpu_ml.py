@@ -169,18 +169,25 @@ def test_mc_ml_ensemble_counters_match_oracle():
 
 
 def test_device_ensemble_ml_ber_matches_reference_plots():
-    """As tests/test_ml_oracle.py, with 40x the trials on the device."""
-    _torch()
-    from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
-    plotted = {0.30: 7.533780499659765e-4, 0.35: 5.9553e-3, 0.40: 4.5414847161572056e-2}
-    for eps, ref in plotted.items():
-        mc = MonteCarlo.ensemble(100, 3, 6, "bec", eps, 1, seed=17, batch=65536, optimal=True,
-                                 message_passing=False)
+    """As tests/test_ml_oracle.py, with 40x the trials on the device (per-trial counts
+    come back from ldpc_ml_ensemble_decode_dev for the variance estimate)."""
+    torch = _torch()
+    from iib_project_ldpc_codes_amd import _native, decoder
+    from tests.test_ml_oracle import PLOTTED_ML_BER_N100, ml_ber_agrees
+    n, B = 100, 65536
+    chk = torch.empty((B, 300), dtype=torch.int32, device="cuda")
+    var = torch.empty_like(chk)
+    for eps in sorted(PLOTTED_ML_BER_N100):
+        counts = []
         for r in range(8):
-            mc.run_batch(r * 65536, 65536, 0)
-        res = mc.results()
-        assert res["num_tests"] == 8 * 65536
-        assert abs(res["ml_ber"] - ref) / ref < 0.2, (eps, res["ml_ber"], ref)
+            rc = _native.lib().ldpc_sample_regular_dev(n, 3, 6, 17, r * B, B, chk.data_ptr(), var.data_ptr(), None,
+                                                       torch.cuda.current_stream().cuda_stream)
+            _native.check(rc, "ldpc_sample_regular_dev")
+            w = decoder.channel_dev("bec", eps, 17, r * B, n, B)
+            _, uns = decoder.ml_ensemble_decode_dev(n, 3, 6, chk, w)
+            counts.append(uns.cpu().numpy())
+        ok, ber, ref = ml_ber_agrees(np.concatenate(counts).astype(np.float64), n, eps)
+        assert ok, (eps, ber, ref)
 
 
 def test_simulator_mirror_optimal_modes(tmp_path, monkeypatch):
