@@ -995,8 +995,8 @@ __global__ __launch_bounds__(256) void mc_reduce_kernel(const int32_t *trial, co
 // columns that are still unknown, target = parity of the known 1-bits of each
 // active check), so elimination needs no LDS for the matrix: per column j one
 // ballot + LDS atomicMin finds the pivot row (first position >= j with bit j set,
-// galois' choice), the pivot row is broadcast through LDS (double-buffered by
-// column parity, two barriers per column), rows p and q swap through LDS, and
+// galois' choice); each wave's first candidate row is staged in LDS before the
+// barrier, so one barrier per column suffices; rows p and q swap through LDS, and
 // every other row holding bit j XORs the pivot in (Gauss-Jordan, above and below).
 // Because the reference looks for the FIRST column whose diagonal entry of the
 // reduced matrix is not 1, elimination stops at the first column without a pivot
@@ -1008,7 +1008,7 @@ __global__ __launch_bounds__(256) void mc_reduce_kernel(const int32_t *trial, co
 // checks are returned unchanged (:66-70).  m <= 1000 (the 1000-unknown cap of
 // :96 can then never bind); n <= 32767.
 //
-// Per-word LDS (dynamic): piv[2][W], swp[W] (u64); best[2], wsum[16] (int);
+// Per-word LDS (dynamic): cand[2][T/64][W], swp[2][W] (u64); best[3], wsum[16] (int);
 // code[n] (int16: column of an active unknown, -1/-2 known 0/1, -3 given up);
 // state[n] (u8: 0/1 known, 2 unknown, 3 given up, 4/5 solved 0/1);
 // rowchk[m], colvar[m] (int16); achk[m] (u8).
@@ -1040,10 +1040,11 @@ __global__ __launch_bounds__(1024) void ml_kernel(const int32_t *__restrict__ cp
                                                   const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
                                                   int32_t *__restrict__ unsolved) {
     extern __shared__ __align__(16) unsigned char ml_lds[];
-    uint64_t *piv = reinterpret_cast<uint64_t *>(ml_lds);  // [2][W]
-    uint64_t *swp = piv + 2 * W;                            // [W]
-    int *best = reinterpret_cast<int *>(swp + W);           // [2]
-    int *wsum = best + 2;                                   // [16]
+    const int NW = blockDim.x >> 6;
+    uint64_t *cand = reinterpret_cast<uint64_t *>(ml_lds);  // [2][NW][W] each wave's first candidate row
+    uint64_t *swp = cand + 2 * NW * W;                       // [2][W] row at the pivot position
+    int *best = reinterpret_cast<int *>(swp + 2 * W);        // [3]
+    int *wsum = best + 3;                                    // [16]
     int16_t *code = reinterpret_cast<int16_t *>(wsum + 16); // [n]
     int16_t *rowchk = code + n;                             // [m]
     int16_t *colvar = rowchk + m;                           // [m]
@@ -1064,7 +1065,7 @@ __global__ __launch_bounds__(1024) void ml_kernel(const int32_t *__restrict__ cp
         ne_local += (x == 2);
     }
     for (int c = tid; c < m; c += T) achk[c] = 1;
-    if (tid < 2) best[tid] = INT_MAX;
+    if (tid < 3) best[tid] = INT_MAX;
     int ne = 0;
     (void)block_excl_scan(ne_local, wsum, ne);  // (its barriers also publish state / achk / best)
     if (ne == 0 || ne > m) {
@@ -1123,50 +1124,53 @@ __global__ __launch_bounds__(1024) void ml_kernel(const int32_t *__restrict__ cp
             if (tgt) ml_set_bit<W>(R, ncols);
         }
         // --- Gauss-Jordan in galois' pivot order until the first column without a pivot.
-        // Window: R[0] holds columns [64*shift, 64*shift+64) of the row.
-        int free_col = -1, shift = 0;
+        // Window: R[0] holds columns [64*shift, 64*shift+64) of the row.  One barrier
+        // per column: every wave's first candidate row is published before the barrier
+        // (with the row at the pivot position, for the swap), so the winner's row is
+        // already in LDS once the pivot position is known.  cand/swp are double-
+        // buffered by column parity, best[] triple-buffered (the atomicMin of column
+        // j+1 may run before a slow thread reads best[] of column j).
+        int free_col = -1, shift = 0, b3 = 0;
         for (int j = 0; j < ncols; ++j) {
             const int buf = j & 1;
             if ((j >> 6) != shift) {
                 ml_shift<W>(R);
                 ++shift;
             }
-            const int live = W - shift;  // words still in the window (uniform)
+            // all W words move every time (no per-word predicates: words past the
+            // window are zero in every row), so the column step is branch-free
             const bool bit = (R[0] >> (j & 63)) & 1ull;
             const uint64_t bal = __ballot(bit && tid >= j && tid < nrows);
-            if (lane == 0 && bal) atomicMin(&best[buf], wave * 64 + (int)__ffsll((long long)bal) - 1);
+            if (bal && lane == (int)__ffsll((long long)bal) - 1) {
+                uint64_t *cw = cand + (buf * NW + wave) * W;
+#pragma unroll
+                for (int w = 0; w < W; ++w) cw[w] = R[w];
+                atomicMin(&best[b3], tid);
+            }
+            if (tid == j) {
+#pragma unroll
+                for (int w = 0; w < W; ++w) swp[buf * W + w] = R[w];
+            }
             __syncthreads();
-            const int q = best[buf];
-            if (tid == 0) best[buf ^ 1] = INT_MAX;
+            const int q = best[b3];
+            const int b_old = b3 == 0 ? 2 : b3 - 1;  // buffer of column j-1 == column j+2
+            if (tid == 0) best[b_old] = INT_MAX;
+            b3 = b3 == 2 ? 0 : b3 + 1;
             if (q == INT_MAX) {
                 free_col = j;
                 break;
             }
-            uint64_t *pb = piv + buf * W;
-            if (tid == q) {
+            const uint64_t *pb = cand + (buf * NW + (q >> 6)) * W;
+            const bool take = (tid == j) && (q != j);           // row j becomes the pivot row
+            const uint64_t msk = (bit && tid != q) ? ~0ull : 0ull;  // rows holding bit j XOR it in
 #pragma unroll
-                for (int w = 0; w < W; ++w)
-                    if (w < live) pb[w] = R[w];
-            } else if (tid == j) {
-#pragma unroll
-                for (int w = 0; w < W; ++w)
-                    if (w < live) swp[w] = R[w];
+            for (int w = 0; w < W; ++w) {
+                const uint64_t pw = pb[w];
+                R[w] = take ? pw : (R[w] ^ (pw & msk));
             }
-            __syncthreads();
-            if (tid == q) {
-                if (q != j) {
+            if (tid == q && q != j) {  // the old row j moves to position q
 #pragma unroll
-                    for (int w = 0; w < W; ++w)
-                        if (w < live) R[w] = swp[w];
-                }
-            } else if (tid == j) {
-#pragma unroll
-                for (int w = 0; w < W; ++w)
-                    if (w < live) R[w] = pb[w];
-            } else if (bit) {
-#pragma unroll
-                for (int w = 0; w < W; ++w)
-                    if (w < live) R[w] ^= pb[w];
+                for (int w = 0; w < W; ++w) R[w] = swp[buf * W + w];
             }
         }
         if (free_col < 0) {
@@ -1510,8 +1514,8 @@ hipError_t launch_mc_reduce(const int32_t *trial, const int32_t *trial_its, int 
     return hipGetLastError();
 }
 
-size_t ml_lds_bytes(int n, int m, int W) {
-    return (size_t)8 * 3 * W + 4 * 18 + (size_t)2 * n + (size_t)4 * m + (size_t)n + (size_t)m + 16;
+size_t ml_lds_bytes(int n, int m, int W, int T) {
+    return (size_t)8 * (2 * (T / 64) + 2) * W + 4 * 19 + (size_t)2 * n + (size_t)4 * m + (size_t)n + (size_t)m + 16;
 }
 
 int ml_words(int m) {
@@ -1526,7 +1530,7 @@ hipError_t launch_ml_decode(const int32_t *cptr, const int32_t *cvar, int64_t cv
     if (B <= 0) return hipSuccess;
     const int W = ml_words(m);
     const int T = std::min(1024, std::max(64, (m + 63) / 64 * 64));
-    const size_t lds = ml_lds_bytes(n, m, W);
+    const size_t lds = ml_lds_bytes(n, m, W, T);
 #define LDPC_ML_CASE(WW)                                                                                    \
     case WW: {                                                                                              \
         hipError_t e = allow_lds(ml_kernel<WW>, lds);                                                       \
