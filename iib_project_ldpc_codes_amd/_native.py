@@ -67,6 +67,8 @@ def lib():
         "ldpc_sample_regular_dev": ([i, i, i, u64, u64, i, P, P, P, P], i),
         "ldpc_sample_regular": ([i, i, i, u64, u64, i, P, P, P], i),
         "ldpc_mc_ensemble_batch_dev": ([i, i, i, i, f, u64, u64, i, i, i, i64, P, P], i),
+        "ldpc_sample_csr_dev": ([i, i, P, P, u64, u64, i, P, P, P, P], i),
+        "ldpc_sample_csr": ([i, i, P, P, u64, u64, i, P, P, P], i),
         "ldpc_ml_decode_batch_dev": ([P, P, i, P, P, P], i),
         "ldpc_ml_decode_batch": ([P, P, i, P, P], i),
         "ldpc_ml_ensemble_decode_dev": ([i, i, i, P, P, i, P, P, P], i),
@@ -97,4 +99,4 @@ def exported_symbols():
             "ldpc_bp_decode_batch_dev", "ldpc_channel_dev", "ldpc_mc_batch_dev", "ldpc_last_error",
             "ldpc_device_count", "ldpc_set_device", "ldpc_sync", "ldpc_debug_lane_layout", "ldpc_bp_kernel_name", "ldpc_sample_regular_dev",
             "ldpc_sample_regular", "ldpc_mc_ensemble_batch_dev", "ldpc_ml_decode_batch_dev", "ldpc_ml_decode_batch",
-            "ldpc_ml_ensemble_decode_dev", "ldpc_mc_ml_batch_dev"]
+            "ldpc_ml_ensemble_decode_dev", "ldpc_mc_ml_batch_dev", "ldpc_sample_csr_dev", "ldpc_sample_csr"]

@@ -39,7 +39,7 @@ struct DevBuf {
 };
 
 struct Workspace {
-    DevBuf trial, its, cutoff, scratch, words, llr, post, hard, errors, itsb, gchk, gvar, gatt, mlw, mlo, mlu;
+    DevBuf trial, its, cutoff, scratch, words, llr, post, hard, errors, itsb, gchk, gvar, gatt, mlw, mlo, mlu, shape;
 };
 std::map<std::pair<int, void *>, Workspace> g_ws;  // (device, stream)
 
@@ -672,6 +672,72 @@ int ldpc_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_gra
     LDPC_HIP(hipDeviceSynchronize());
     LDPC_HIP(hipMemcpy(check_lookup, ws.gchk.p, E * G * 4, hipMemcpyDeviceToHost));
     LDPC_HIP(hipMemcpy(variable_lookup, ws.gvar.p, E * G * 4, hipMemcpyDeviceToHost));
+    if (attempts) LDPC_HIP(hipMemcpy(attempts, ws.gatt.p, (size_t)G * 4, hipMemcpyDeviceToHost));
+    return LDPC_OK;
+}
+
+// Irregular configuration model: degree structure (host arrays) -> device shape buffer
+// [vsock E | cptr m+1 | vptr n+1] on the workspace of `stream` (caller holds g_mu).
+static int csr_shape_upload(int n, int m, const int32_t *var_ptr, const int32_t *check_ptr, Workspace &ws,
+                            int *E_out, const int32_t **vsock, const int32_t **cptr, const int32_t **vptr) {
+    LDPC_REQUIRE(n > 0 && m > 0 && var_ptr && check_ptr, "bad degree structure");
+    LDPC_REQUIRE(var_ptr[0] == 0 && check_ptr[0] == 0, "var_ptr / check_ptr must start at 0");
+    for (int v = 0; v < n; ++v) LDPC_REQUIRE(var_ptr[v + 1] >= var_ptr[v], "var_ptr must be non-decreasing");
+    for (int c = 0; c < m; ++c) LDPC_REQUIRE(check_ptr[c + 1] >= check_ptr[c], "check_ptr must be non-decreasing");
+    const int E = var_ptr[n];
+    LDPC_REQUIRE(E > 0 && E == check_ptr[m], "socket counts differ: var_ptr[n] != check_ptr[m]");
+    std::vector<int32_t> h((size_t)E + m + 1 + n + 1);
+    for (int v = 0; v < n; ++v)
+        for (int e = var_ptr[v]; e < var_ptr[v + 1]; ++e) h[e] = v;
+    std::copy(check_ptr, check_ptr + m + 1, h.begin() + E);
+    std::copy(var_ptr, var_ptr + n + 1, h.begin() + E + m + 1);
+    LDPC_HIP(ws.shape.ensure(h.size() * 4));
+    LDPC_HIP(hipMemcpy(ws.shape.p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    const int32_t *base = static_cast<const int32_t *>(ws.shape.p);
+    *E_out = E;
+    *vsock = base;
+    *cptr = base + E;
+    *vptr = base + E + m + 1;
+    return LDPC_OK;
+}
+
+int ldpc_sample_csr_dev(int n, int m, const int32_t *var_ptr, const int32_t *check_ptr, uint64_t seed,
+                        uint64_t first_graph, int G, int32_t *d_check_var, int32_t *d_var_slot, int32_t *d_attempts,
+                        void *stream) {
+    LDPC_REQUIRE(d_check_var && d_var_slot && G >= 0, "bad sampler arguments");
+    int rc = require_device();
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(g_mu);
+    Workspace &ws = workspace(stream);
+    int E = 0;
+    const int32_t *vs, *cp, *vp;
+    rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, &E, &vs, &cp, &vp);
+    if (rc) return rc;
+    LDPC_HIP(launch_sample_csr(n, m, E, vs, cp, vp, seed, first_graph, G, d_check_var, d_var_slot, d_attempts,
+                               1 << 20, static_cast<hipStream_t>(stream)));
+    return LDPC_OK;
+}
+
+int ldpc_sample_csr(int n, int m, const int32_t *var_ptr, const int32_t *check_ptr, uint64_t seed,
+                    uint64_t first_graph, int G, int32_t *check_var, int32_t *var_slot, int32_t *attempts) {
+    LDPC_REQUIRE(check_var && var_slot && G >= 0, "bad sampler arguments");
+    int rc = require_device();
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(g_mu);
+    Workspace &ws = workspace(nullptr);
+    int E = 0;
+    const int32_t *vs, *cp, *vp;
+    rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, &E, &vs, &cp, &vp);
+    if (rc) return rc;
+    LDPC_HIP(ws.gchk.ensure((size_t)E * G * 4));
+    LDPC_HIP(ws.gvar.ensure((size_t)E * G * 4));
+    LDPC_HIP(ws.gatt.ensure((size_t)G * 4 + 4));
+    LDPC_HIP(launch_sample_csr(n, m, E, vs, cp, vp, seed, first_graph, G, static_cast<int32_t *>(ws.gchk.p),
+                               static_cast<int32_t *>(ws.gvar.p), static_cast<int32_t *>(ws.gatt.p), 1 << 20,
+                               nullptr));
+    LDPC_HIP(hipDeviceSynchronize());
+    LDPC_HIP(hipMemcpy(check_var, ws.gchk.p, (size_t)E * G * 4, hipMemcpyDeviceToHost));
+    LDPC_HIP(hipMemcpy(var_slot, ws.gvar.p, (size_t)E * G * 4, hipMemcpyDeviceToHost));
     if (attempts) LDPC_HIP(hipMemcpy(attempts, ws.gatt.p, (size_t)G * 4, hipMemcpyDeviceToHost));
     return LDPC_OK;
 }

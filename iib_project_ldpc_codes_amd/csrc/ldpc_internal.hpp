@@ -90,6 +90,11 @@ inline int sample_buckets(int E) { return E <= 16384 ? 256 : (E < 65536 ? 512 : 
 hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
                                  int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts,
                                  int max_attempts, hipStream_t stream);
+// Irregular form: socket s of variable d_vsock[s]; check c owns slots [cptr[c], cptr[c+1]);
+// outputs check_var[g][E] and var_slot[g][E] (CSR, each variable's slots ascending).
+hipError_t launch_sample_csr(int n, int m, int E, const int32_t *d_vsock, const int32_t *d_cptr,
+                             const int32_t *d_vptr, uint64_t seed, uint64_t first_graph, int G, int32_t *check_var,
+                             int32_t *var_slot, int32_t *attempts, int max_attempts, hipStream_t stream);
 // BEC Monte-Carlo where trial b decodes on graph b of (check_lookup, variable_lookup).
 hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,
                                   float p, uint64_t seed, uint64_t first_cw, int B, int max_iters, int32_t *trial,

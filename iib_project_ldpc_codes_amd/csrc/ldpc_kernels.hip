@@ -702,8 +702,19 @@ struct BucketRng {  // sequential Philox stream of one bucket
     }
 };
 
+// Degree structure: regular (vsock == nullptr: socket s belongs to variable s/dv,
+// check c owns slots [c*dc, c*dc+dc)) or CSR (vsock[s] = variable of socket s,
+// check c owns slots [cptr[c], cptr[c+1])).  Output, per graph: the variable of
+// every slot (check_lookup / CSR check_var) and the variable side -- regular:
+// variable_lookup[v*dv + k] = k-th check of v (ascending); CSR: var_slot[vptr[v]
+// + k] = k-th slot of v (ascending).
+struct SampleShape {
+    int n, m, E, dv, dc;
+    const int32_t *vsock, *cptr, *vptr;
+};
+
 template <int T, typename Idx, bool LDSBUF>
-__global__ __launch_bounds__(T) void sample_regular_kernel(int n, int dv, int dc, uint32_t k0, uint32_t k1,
+__global__ __launch_bounds__(T) void sample_regular_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
                                                            uint64_t first_graph, int32_t *check_lookup,
                                                            int32_t *variable_lookup, int32_t *attempts,
                                                            int max_attempts) {
@@ -712,7 +723,8 @@ __global__ __launch_bounds__(T) void sample_regular_kernel(int n, int dv, int dc
     extern __shared__ __align__(16) unsigned char smem[];
     int *cnt = reinterpret_cast<int *>(smem);  // [T buckets][NW waves]
     int *wsum = cnt + T * NW;                  // [16]
-    const int E = n * dv, m = E / dc;
+    const int n = sh.n, E = sh.E, m = sh.m, dv = sh.dv, dc = sh.dc;
+    const bool csr = sh.vsock != nullptr;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t gid = first_graph + blockIdx.x;
     const uint32_t g0 = (uint32_t)gid, g1 = (uint32_t)(gid >> 32);
@@ -780,7 +792,7 @@ __global__ __launch_bounds__(T) void sample_regular_kernel(int n, int dv, int dc
                 if (group(base, r, bk, peers)) {
                     const int s = base + lane;
                     const int dst = cnt[bk * NW + wave] + __popcll(peers & lt_mask);
-                    buf[dst] = (Idx)(s / dv);
+                    buf[dst] = (Idx)(csr ? sh.vsock[s] : s / dv);
                     if ((peers & lt_mask) == 0) cnt[bk * NW + wave] += __popcll(peers);
                 }
             }
@@ -801,9 +813,10 @@ __global__ __launch_bounds__(T) void sample_regular_kernel(int n, int dv, int dc
         // 3. every check simple?
         int bad = 0;
         for (int c = tid; c < m; c += T) {
-            const Idx *r = buf + (size_t)c * dc;
-            for (int x = 0; x < dc && !bad; ++x)
-                for (int y = x + 1; y < dc; ++y) bad |= (r[x] == r[y]);
+            const int lo = csr ? sh.cptr[c] : c * dc, d = csr ? sh.cptr[c + 1] - lo : dc;
+            const Idx *r = buf + lo;
+            for (int x = 0; x < d && !bad; ++x)
+                for (int y = x + 1; y < d; ++y) bad |= (r[x] == r[y]);
         }
         ok = !__syncthreads_or(bad);
         ++att;
@@ -824,16 +837,19 @@ __global__ __launch_bounds__(T) void sample_regular_kernel(int n, int dv, int dc
     __threadfence_block();
     __syncthreads();
     for (int x = tid; x < E; x += T) {
-        int32_t *row = vl + (size_t)buf[x] * dv;
-        const int c = x / dc;
-        for (int k = 0; k < dv; ++k)
-            if (atomicCAS(&row[k], -1, c) == -1) break;
+        const int v = buf[x];
+        int32_t *row = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
+        const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
+        const int val = csr ? x : x / dc;
+        for (int k = 0; k < deg; ++k)
+            if (atomicCAS(&row[k], -1, val) == -1) break;
     }
     __threadfence_block();
     __syncthreads();
     for (int v = tid; v < n; v += T) {
-        int32_t *r = vl + (size_t)v * dv;
-        for (int x = 1; x < dv; ++x) {
+        int32_t *r = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
+        const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
+        for (int x = 1; x < deg; ++x) {
             const int key = r[x];
             int y = x - 1;
             while (y >= 0 && r[y] > key) {
@@ -1455,28 +1471,43 @@ hipError_t launch_mc_decode(const ldpc_graph &g, int channel, float p, float p2,
     return dispatch_bp_algo<true>(g, a, algo, early_stop, stream);
 }
 
-hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
-                                 int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts,
-                                 int max_attempts, hipStream_t stream) {
+static hipError_t launch_sample(const SampleShape &sh, uint64_t seed, uint64_t first_graph, int G,
+                                int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts, int max_attempts,
+                                hipStream_t stream) {
     if (G <= 0) return hipSuccess;
-    const int E = n * dv;
+    const int E = sh.E;
     const int K = sample_buckets(E);
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     const size_t ctl = (size_t)4 * (K * (K / kWave) + 16);
+    const bool u16 = sh.n <= 65536;
 #define LDPC_SAMPLE(TT, IDX, LDSB)                                                                             \
     do {                                                                                                       \
         auto k = sample_regular_kernel<TT, IDX, LDSB>;                                                         \
         const size_t lds = ctl + (LDSB ? (size_t)2 * E : 0);                                                   \
         hipError_t e = allow_lds(k, lds);                                                                      \
         if (e != hipSuccess) return e;                                                                         \
-        hipLaunchKernelGGL(k, dim3(G), dim3(TT), lds, stream, n, dv, dc, k0, k1, first_graph, check_lookup,    \
+        hipLaunchKernelGGL(k, dim3(G), dim3(TT), lds, stream, sh, k0, k1, first_graph, check_lookup,           \
                            variable_lookup, attempts, max_attempts);                                           \
         return hipGetLastError();                                                                              \
     } while (0)
-    if (K == 256) LDPC_SAMPLE(256, uint16_t, true);
-    if (K == 512) LDPC_SAMPLE(512, uint16_t, true);
+    if (K == 256 && u16) LDPC_SAMPLE(256, uint16_t, true);
+    if (K == 512 && u16) LDPC_SAMPLE(512, uint16_t, true);
     LDPC_SAMPLE(1024, int32_t, false);
 #undef LDPC_SAMPLE
+}
+
+hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
+                                 int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts,
+                                 int max_attempts, hipStream_t stream) {
+    const SampleShape sh{n, n * dv / dc, n * dv, dv, dc, nullptr, nullptr, nullptr};
+    return launch_sample(sh, seed, first_graph, G, check_lookup, variable_lookup, attempts, max_attempts, stream);
+}
+
+hipError_t launch_sample_csr(int n, int m, int E, const int32_t *d_vsock, const int32_t *d_cptr,
+                             const int32_t *d_vptr, uint64_t seed, uint64_t first_graph, int G, int32_t *check_var,
+                             int32_t *var_slot, int32_t *attempts, int max_attempts, hipStream_t stream) {
+    const SampleShape sh{n, m, E, 0, 0, d_vsock, d_cptr, d_vptr};
+    return launch_sample(sh, seed, first_graph, G, check_var, var_slot, attempts, max_attempts, stream);
 }
 
 hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,

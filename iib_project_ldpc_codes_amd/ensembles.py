@@ -120,6 +120,36 @@ def sample_irregular(ens, n, seed=0, max_retries=100000, deg2="random", min_cycl
     return TannerGraph.from_csr(cptr, cvar.astype(np.int32), vptr, vslot)
 
 
+def degree_ptrs(ens, n):
+    """(var_ptr, check_ptr) of the degree sequences (sockets of variable v at
+    var_ptr[v].., slots of check c at check_ptr[c]..)."""
+    vdeg, cdeg = degree_sequences(ens, n)
+    vptr = np.zeros(n + 1, np.int32)
+    vptr[1:] = np.cumsum(vdeg)
+    cptr = np.zeros(cdeg.size + 1, np.int32)
+    cptr[1:] = np.cumsum(cdeg)
+    return vptr, cptr
+
+
+def sample_irregular_device(ens, n, seed=0, graph_id=0):
+    """Graph `graph_id` of the on-device sampler (ldpc_sample_csr): the law of
+    sample_irregular(deg2="random") -- uniform socket matching, whole-graph redraw
+    while a check holds a variable twice -- drawn by the same counter-based
+    generator as the regular device sampler (any graph can be regenerated)."""
+    from . import _native
+    vptr, cptr = degree_ptrs(ens, n)
+    E = int(vptr[-1])
+    cvar = np.zeros(E, np.int32)
+    vslot = np.zeros(E, np.int32)
+    att = np.zeros(1, np.int32)
+    rc = _native.lib().ldpc_sample_csr(n, len(cptr) - 1, vptr.ctypes.data, cptr.ctypes.data, int(seed),
+                                       int(graph_id), 1, cvar.ctypes.data, vslot.ctypes.data, att.ctypes.data)
+    _native.check(rc, "ldpc_sample_csr")
+    if att[0] <= 0:
+        raise RuntimeError("sampler hit its attempt cap")
+    return TannerGraph.from_csr(cptr, cvar, vptr, vslot)
+
+
 def _csr_from_pairs(n, m, cdeg, var_check_pairs):
     """CSR slot form from (variable, check) edge pairs; slots check-major, each check's
     variables in the pair order, each variable's edges in ascending check order."""

@@ -170,6 +170,23 @@ int ldpc_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_gra
                         int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts);
 
 /*
+ * Irregular form (the same law for any degree structure): n
+ * variables with var_ptr[v+1]-var_ptr[v] sockets each, m checks with
+ * check_ptr[c+1]-check_ptr[c] slots each (host arrays, var_ptr[n] ==
+ * check_ptr[m] == E); a uniformly random socket->slot matching, redrawn whole
+ * while any check holds a variable twice.  Output per graph g (row-major):
+ * check_var int32[G][E] (variable of each slot, check-major) and var_slot
+ * int32[G][E] (for variable v, entries var_ptr[v].. = its slots ascending) --
+ * the ldpc_graph_create_csr layout.  Same generator as ldpc_sample_regular
+ * (which is this with var_ptr = v*dv, check_ptr = c*dc, var_slot -> check ids).
+ */
+int ldpc_sample_csr_dev(int n, int m, const int32_t *var_ptr, const int32_t *check_ptr, uint64_t seed,
+                        uint64_t first_graph, int G, int32_t *d_check_var, int32_t *d_var_slot, int32_t *d_attempts,
+                        void *stream);
+int ldpc_sample_csr(int n, int m, const int32_t *var_ptr, const int32_t *check_ptr, uint64_t seed,
+                    uint64_t first_graph, int G, int32_t *check_var, int32_t *var_slot, int32_t *attempts);
+
+/*
  * Ensemble BEC Monte-Carlo batch (run_simulation, parallel_simulator.py:168-272;
  * expurgated :169-285): trial t = first_cw + b draws graph t and channel word t,
  * decodes with message_passing semantics and accumulates counters exactly as

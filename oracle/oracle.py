@@ -54,6 +54,8 @@ def lib():
         _lib.oracle_ml_decode_batch.restype = None
         _lib.oracle_sample_regular_batch.argtypes = [i, i, i, u64, u64, i, i, P, P, P]
         _lib.oracle_sample_regular_batch.restype = None
+        _lib.oracle_sample_csr.argtypes = [i, i, P, P, u64, u64, i, P, P]
+        _lib.oracle_sample_csr.restype = i
         _lib.oracle_num_threads.argtypes = []
         _lib.oracle_num_threads.restype = i
     return _lib
@@ -162,6 +164,17 @@ def sample_regular_batch(n, dv, dc, seed, first_graph, G, max_attempts=1 << 20):
     att = np.zeros(G, np.int32)
     lib().oracle_sample_regular_batch(n, dv, dc, seed, first_graph, G, max_attempts, _p(chk), _p(var), _p(att))
     return chk, var, att
+
+
+def sample_csr(var_ptr, check_ptr, seed, graph, max_attempts=1 << 20):
+    """Irregular form of the device sampler.  Returns (check_var [E], var_slot [E], attempts)."""
+    vp = np.ascontiguousarray(var_ptr, np.int32)
+    cp = np.ascontiguousarray(check_ptr, np.int32)
+    n, m, E = len(vp) - 1, len(cp) - 1, int(vp[-1])
+    cv = np.zeros(E, np.int32)
+    vs = np.zeros(E, np.int32)
+    att = lib().oracle_sample_csr(n, m, _p(vp), _p(cp), seed, graph, max_attempts, _p(cv), _p(vs))
+    return cv, vs, att
 
 
 def density_evolution(eps, iterations, dv, dc, threshold=0.0):

@@ -67,3 +67,55 @@ def test_zigzag_construction_preserves_degrees_and_removes_weight2():
         p = tuple(sorted(slot_check[vslot[vptr[v]:vptr[v + 1]]]))
         assert p not in pairs
         pairs.add(p)
+
+
+def test_oracle_csr_sampler_regular_structure_equals_regular_sampler():
+    """ldpc_sample_csr with v*dv / c*dc pointers is the regular generator."""
+    from oracle import oracle
+    n, dv, dc = 300, 3, 6
+    vptr = np.arange(n + 1, dtype=np.int32) * dv
+    cptr = np.arange(n * dv // dc + 1, dtype=np.int32) * dc
+    for g in range(5):
+        chk, var, att = oracle.sample_regular(n, dv, dc, 9, g)
+        cv, vs, att2 = oracle.sample_csr(vptr, cptr, 9, g)
+        assert att == att2
+        np.testing.assert_array_equal(cv, chk)
+        np.testing.assert_array_equal(vs // dc, var)  # slots -> checks
+
+
+def test_oracle_csr_sampler_irregular_law():
+    """Irregular RSU graphs: degrees as specified, no check holds a variable twice,
+    variable side consistent, and the 4-cycle statistic matches the host
+    configuration-model sampler (same law, different generator)."""
+    from oracle import oracle
+    from iib_project_ldpc_codes_amd import ensembles
+    n = 200
+    vptr, cptr = ensembles.degree_ptrs(ensembles.RSU_DL4, n)
+    m = len(cptr) - 1
+
+    def four_cycles(cp, cv):
+        H = np.zeros((m, n), np.int32)
+        for c in range(m):
+            H[c, cv[cp[c]:cp[c + 1]]] = 1
+        O = H @ H.T
+        np.fill_diagonal(O, 0)
+        return (O * (O - 1) // 2).sum() // 2
+
+    dev, host = [], []
+    for g in range(400):
+        cv, vs, att = oracle.sample_csr(vptr, cptr, 4, g)
+        assert att > 0
+        for c in range(m):
+            row = cv[cptr[c]:cptr[c + 1]]
+            assert len(set(row.tolist())) == len(row)
+        assert np.array_equal(np.bincount(cv, minlength=n), np.diff(vptr))
+        for v in (0, n // 2, n - 1):
+            sl = vs[vptr[v]:vptr[v + 1]]
+            assert np.all(cv[sl] == v) and np.all(np.diff(sl) > 0)
+        dev.append(four_cycles(cptr, cv))
+        hg = ensembles.sample_irregular(ensembles.RSU_DL4, n, seed=g)
+        hcp, hcv, _, _ = hg.to_csr()
+        host.append(four_cycles(hcp, hcv))
+    dev, host = np.array(dev, float), np.array(host, float)
+    se = np.sqrt(dev.var() / len(dev) + host.var() / len(host))
+    assert abs(dev.mean() - host.mean()) < 4 * se

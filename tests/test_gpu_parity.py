@@ -376,7 +376,7 @@ def test_parallel_simulator_per_trial_engine(torch, tmp_path, monkeypatch):
 
 
 # ------------------------------------------------------------ random graphs
-@pytest.mark.parametrize("n,dv,dc", [(1000, 3, 6), (90, 2, 3), (96, 4, 8), (10000, 3, 6)])
+@pytest.mark.parametrize("n,dv,dc", [(1000, 3, 6), (90, 2, 3), (96, 4, 8), (10000, 3, 6), (30000, 3, 6)])
 def test_device_sampler_matches_oracle(torch, n, dv, dc):
     from iib_project_ldpc_codes_amd import _native
     L = _native.lib()
@@ -391,6 +391,33 @@ def test_device_sampler_matches_oracle(torch, n, dv, dc):
         assert att[g] == oatt > 0
         np.testing.assert_array_equal(chk[g * E:(g + 1) * E], ochk)
         np.testing.assert_array_equal(var[g * E:(g + 1) * E], ovar)
+
+
+@pytest.mark.parametrize("n", [2000, 20000, 30000])
+def test_device_irregular_sampler_matches_oracle(torch, n):
+    """ldpc_sample_csr (RSU rate-1/2 degree structure) == oracle_sample_csr, bit for bit;
+    n = 2000 / 20000 use the LDS permutation (256 / 512 buckets), 30000 the global one."""
+    from iib_project_ldpc_codes_amd import _native, ensembles
+    vptr, cptr = ensembles.degree_ptrs(ensembles.RSU_DL4, n)
+    E, m, G = int(vptr[-1]), len(cptr) - 1, 4
+    cv = np.zeros(G * E, np.int32)
+    vs = np.zeros(G * E, np.int32)
+    att = np.zeros(G, np.int32)
+    rc = _native.lib().ldpc_sample_csr(n, m, vptr.ctypes.data, cptr.ctypes.data, 8, 50, G, cv.ctypes.data,
+                                       vs.ctypes.data, att.ctypes.data)
+    assert rc == 0
+    for g in range(G):
+        ocv, ovs, oatt = oracle.sample_csr(vptr, cptr, 8, 50 + g)
+        assert att[g] == oatt > 0
+        np.testing.assert_array_equal(cv[g * E:(g + 1) * E], ocv)
+        np.testing.assert_array_equal(vs[g * E:(g + 1) * E], ovs)
+    # a sampled irregular graph decodes like its oracle (min-sum is bit-exact)
+    from iib_project_ldpc_codes_amd import decoder
+    g = ensembles.sample_irregular_device(ensembles.RSU_DL4, n, seed=8, graph_id=50)
+    llr = oracle.channel(oracle.CH_AWGN, 0.8, 3, 0, n, 8)
+    _, hard, its = decoder.bp_decode(g, llr, 20, "minsum", alpha=0.75)
+    _, ohard, _ = oracle.bp_decode_batch(g.to_csr(), llr, 20, 1, alpha=0.75)
+    np.testing.assert_array_equal(hard, ohard)
 
 
 def test_ensemble_mc_matches_oracle(torch):
