@@ -31,12 +31,18 @@ struct ldpc_graph {
 };
 
 // Threads per workgroup and variables per thread of the LDS-resident kernel
-// for block length n: >= 3 % spare lanes so the layout can avoid LDS bank
-// conflicts.  Must match the instantiations in ldpc_kernels.hip.
+// for block length n: >= 2 % spare lanes for the conflict-aware layout.  (At
+// n = 10^4, 3 % spare = 11 variables per thread packs with ~1.02 LDS cycles per
+// half-wave access, 2 % = 10 per thread with ~1.5 -- and is 5 % faster: the
+// variable phase is bound by per-lane work, not bank conflicts.)  Must match the
+// instantiations in ldpc_kernels.hip.
+#ifndef LDPC_LDS_SPARE
+#define LDPC_LDS_SPARE 102  // lanes >= n * SPARE / 100 (fewer lanes beat fewer bank conflicts)
+#endif
 inline bool lds_shape(int n, int &T, int &VPT) {
     static const int v256[] = {1, 2, 3, 5, 9};
-    static const int v1024[] = {2, 3, 5, 6, 9, 11, 14};
-    const long need = ((long)n * 103 + 99) / 100;
+    static const int v1024[] = {2, 3, 5, 6, 9, 10, 11, 14};
+    const long need = ((long)n * LDPC_LDS_SPARE + 99) / 100;
     if (n <= 2048) {
         T = 256;
         for (int v : v256)

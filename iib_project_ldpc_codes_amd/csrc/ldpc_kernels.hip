@@ -35,7 +35,7 @@ constexpr int kWave = 64;
 #define LDPC_SAMPLER_SKIP 0       // timing ablation only: 2 = no Fisher-Yates, 8 = no variable_lookup
 #endif
 #ifndef LDPC_CHECK_UNROLL
-#define LDPC_CHECK_UNROLL 1
+#define LDPC_CHECK_UNROLL 2  // two checks in flight per thread (VGPR budget of 4 waves/SIMD)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -1323,7 +1323,7 @@ hipError_t launch_lds36(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     if (g.lane_T == TT && g.lane_VPT == VV) return launch_lds36_vpt<VV, TT, ALGO, ET, MC>(g, a, lds, s);
     LDS36_CASE(256, 1) LDS36_CASE(256, 2) LDS36_CASE(256, 3) LDS36_CASE(256, 5) LDS36_CASE(256, 9)
     LDS36_CASE(1024, 2) LDS36_CASE(1024, 3) LDS36_CASE(1024, 5) LDS36_CASE(1024, 6) LDS36_CASE(1024, 9)
-    LDS36_CASE(1024, 11) LDS36_CASE(1024, 14)
+    LDS36_CASE(1024, 10) LDS36_CASE(1024, 11) LDS36_CASE(1024, 14)
 #undef LDS36_CASE
     return hipErrorInvalidValue;
 }
