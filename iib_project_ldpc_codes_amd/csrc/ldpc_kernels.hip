@@ -713,6 +713,206 @@ struct SampleShape {
     const int32_t *vsock, *cptr, *vptr;
 };
 
+// Variable side of a sampled graph from its check side (chk[x] = variable of
+// slot x, global): regular rows get check ids, CSR rows slot ids, each row
+// ascending (claims by atomic CAS, then a per-row insertion sort).
+__device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, int32_t *vl) {
+    const int tid = threadIdx.x, T = blockDim.x;
+    const int n = sh.n, E = sh.E, dv = sh.dv, dc = sh.dc;
+    const bool csr = sh.vsock != nullptr;
+    for (int x = tid; x < E; x += T) vl[x] = -1;
+    __threadfence_block();
+    __syncthreads();
+    for (int x = tid; x < E; x += T) {
+        const int v = chk[x];
+        int32_t *row = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
+        const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
+        const int val = csr ? x : x / dc;
+        for (int k = 0; k < deg; ++k)
+            if (atomicCAS(&row[k], -1, val) == -1) break;
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int v = tid; v < n; v += T) {
+        int32_t *r = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
+        const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
+        for (int x = 1; x < deg; ++x) {
+            const int key = r[x];
+            int y = x - 1;
+            while (y >= 0 && r[y] > key) {
+                r[y + 1] = r[y];
+                --y;
+            }
+            r[y + 1] = key;
+        }
+    }
+}
+
+// Large graphs (n*dv >= 65536, n <= 65536): two-level Rao-Sandelius, still
+// exactly uniform.  Level 1 splits all sockets into K1 super-buckets (draws
+// ctr {(s>>8)<<6 | s&63, tag|att<<2|2, g}; stable scatter of variable ids as
+// u16 into the variable_lookup row, used as scratch); super-bucket i is then
+// staged into LDS and permuted by the one-level scheme with 512 buckets (draws
+// ctr {.., tag|i<<22|att<<2|0, g}, Fisher-Yates streams {t<<20|blk,
+// tag|i<<22|att<<2|1, g}) and written to its slot range.  Checks are validated
+// as soon as all their slots are final, so a bad attempt usually stops after a
+// few super-buckets.  A super-bucket larger than the LDS staging capacity
+// (kBigCap, > 2x the mean -- probability < e^-4000 at the sizes that use this
+// path) rejects the attempt.  oracle_sample_regular / oracle_sample_csr restate
+// it bit for bit.
+template <int LOGK1>
+__global__ __launch_bounds__(1024) void sample_big_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
+                                                         uint64_t first_graph, int32_t *check_lookup,
+                                                         int32_t *variable_lookup, int32_t *attempts,
+                                                         int max_attempts) {
+    constexpr int T = 1024, NW = T / kWave, K2 = kBigK2, LOGK2 = 9, K1 = 1 << LOGK1;
+    extern __shared__ __align__(16) unsigned char smem[];
+    int *cnt2 = reinterpret_cast<int *>(smem);  // [K2][NW]
+    int *cnt1 = cnt2 + K2 * NW;                  // [K1][NW]
+    int *wsum = cnt1 + K1 * NW;                  // [16]
+    int *sst = wsum + 16;                        // [K1 + 1] super-bucket starts
+    uint16_t *A = reinterpret_cast<uint16_t *>(sst + 68);
+    uint16_t *Bf = A + kBigCap;
+    const int n = sh.n, E = sh.E, m = sh.m, dv = sh.dv, dc = sh.dc;
+    const bool csr = sh.vsock != nullptr;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t gid = first_graph + blockIdx.x;
+    const uint32_t g0 = (uint32_t)gid, g1 = (uint32_t)(gid >> 32);
+    int32_t *out = check_lookup + (size_t)blockIdx.x * E;
+    uint16_t *L1 = reinterpret_cast<uint16_t *>(variable_lookup + (size_t)blockIdx.x * E);
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    (void)n;
+
+    // one-level pass over [0, S) split into per-wave chunks: bucket of element s from
+    // word (s>>6)&3 of Philox {(s>>8)<<6 | lane, c1, g}, top LOGK bits; f(s, bk, rank, peers)
+    auto pass = [&](int S, uint32_t c1, int logk, auto &&f) {
+        const int chunk = ((S + NW - 1) / NW + 255) / 256 * 256;
+        const int lo = min(S, wave * chunk), hi = min(S, lo + chunk);
+        for (int b256 = lo; b256 < hi; b256 += 256) {
+            const uint4 r = philox_block((uint32_t)(((b256 >> 8) << 6) | lane), c1, g0, g1, k0, k1);
+            for (int base = b256; base < min(hi, b256 + 256); base += 64) {
+                const int s = base + lane;
+                const bool valid = s < hi;
+                const uint32_t bk = valid ? pick4(r, (base >> 6) & 3) >> (32 - logk) : 0u;
+                uint64_t peers = __ballot(valid);
+                for (int bit = 0; bit < logk; ++bit) {
+                    const bool on = (bk >> bit) & 1u;
+                    const uint64_t bal = __ballot(valid && on);
+                    peers &= on ? bal : ~bal;
+                }
+                if (valid) f(s, (int)bk, __popcll(peers & lt_mask), peers);
+            }
+        }
+    };
+    // counts -> offsets, bucket-major / wave-minor; returns this thread's bucket start/size
+    auto offsets = [&](int *cnt, int K, int &start, int &size) {
+        size = 0;
+        if (tid < K)
+            for (int w = 0; w < NW; ++w) size += cnt[tid * NW + w];
+        int total = 0;
+        start = block_excl_scan(size, wsum, total);
+        if (tid < K) {
+            int run = start;
+            for (int w = 0; w < NW; ++w) {
+                const int c = cnt[tid * NW + w];
+                cnt[tid * NW + w] = run;
+                run += c;
+            }
+        }
+        __syncthreads();
+    };
+
+    int att = 0;
+    bool ok = false;
+    while (!ok && att < max_attempts) {
+        const uint32_t ca = kSampleTag | ((uint32_t)att << 2);
+        // ---- level 1
+        for (int i = tid; i < K1 * NW; i += T) cnt1[i] = 0;
+        __syncthreads();
+        pass(E, ca | 2u, LOGK1, [&](int, int bk, int rank, uint64_t peers) {
+            if (rank == 0) cnt1[bk * NW + wave] += __popcll(peers);
+        });
+        __syncthreads();
+        int st1, sz1;
+        offsets(cnt1, K1, st1, sz1);
+        if (tid < K1) sst[tid] = st1;
+        if (tid == 0) sst[K1] = E;
+        pass(E, ca | 2u, LOGK1, [&](int s, int bk, int rank, uint64_t peers) {
+            L1[cnt1[bk * NW + wave] + rank] = (uint16_t)(csr ? sh.vsock[s] : s / dv);
+            if (rank == 0) cnt1[bk * NW + wave] += __popcll(peers);
+        });
+        __threadfence_block();
+        __syncthreads();
+        // ---- level 2, super-bucket by super-bucket, validating finished checks
+        bool bad = false;
+        int done = 0;  // checks validated so far
+        for (int i = 0; i < K1 && !bad; ++i) {
+            const int st = sst[i], S = sst[i + 1] - st;
+            if (S > kBigCap) {
+                bad = true;
+                break;
+            }
+            const uint32_t ci = ca | ((uint32_t)i << 22);
+            for (int x = tid; x < S; x += T) A[x] = L1[st + x];
+            for (int x = tid; x < K2 * NW; x += T) cnt2[x] = 0;
+            __syncthreads();
+            pass(S, ci, LOGK2, [&](int, int bk, int rank, uint64_t peers) {
+                if (rank == 0) cnt2[bk * NW + wave] += __popcll(peers);
+            });
+            __syncthreads();
+            int st2, sz2;
+            offsets(cnt2, K2, st2, sz2);
+            pass(S, ci, LOGK2, [&](int s, int bk, int rank, uint64_t peers) {
+                Bf[cnt2[bk * NW + wave] + rank] = A[s];
+                if (rank == 0) cnt2[bk * NW + wave] += __popcll(peers);
+            });
+            __syncthreads();
+            if (tid < K2 && !(LDPC_SAMPLER_SKIP & 2)) {
+                BucketRng rng{k0, k1, (uint32_t)tid << 20, ci | 1u, g0, g1};
+                uint16_t *bb = Bf + st2;
+                for (int x = sz2 - 1; x >= 1; --x) {
+                    const int j = (int)rng.below((uint32_t)x + 1u);
+                    const uint16_t t = bb[x];
+                    bb[x] = bb[j];
+                    bb[j] = t;
+                }
+            }
+            __syncthreads();
+            for (int x = tid; x < S; x += T) out[st + x] = Bf[x];
+            __threadfence_block();
+            __syncthreads();
+            // checks whose slots all lie below st + S
+            int hi_c;
+            if (csr) {
+                int lo = done, hi = m;  // first c >= done with cptr[c+1] > st + S
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sh.cptr[mid + 1] <= st + S) lo = mid + 1;
+                    else hi = mid;
+                }
+                hi_c = lo;
+            } else {
+                hi_c = (st + S) / dc;
+            }
+            int b = 0;
+            for (int c = done + tid; c < hi_c; c += T) {
+                const int lo = csr ? sh.cptr[c] : c * dc, d = csr ? sh.cptr[c + 1] - lo : dc;
+                const int32_t *r = out + lo;
+                for (int x = 0; x < d && !b; ++x)
+                    for (int y = x + 1; y < d; ++y) b |= (r[x] == r[y]);
+            }
+            done = hi_c;
+            bad = __syncthreads_or(b);
+        }
+        ok = !bad;
+        ++att;
+        if (LDPC_SAMPLER_FIXED_ATT > 0) ok = att >= LDPC_SAMPLER_FIXED_ATT;
+    }
+    if (attempts && tid == 0) attempts[blockIdx.x] = ok ? att : -att;
+    if (LDPC_SAMPLER_SKIP & 8) return;
+    sample_emit_var_side(sh, out, variable_lookup + (size_t)blockIdx.x * E);
+}
+
 template <int T, typename Idx, bool LDSBUF>
 __global__ __launch_bounds__(T) void sample_regular_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
                                                            uint64_t first_graph, int32_t *check_lookup,
@@ -723,7 +923,7 @@ __global__ __launch_bounds__(T) void sample_regular_kernel(SampleShape sh, uint3
     extern __shared__ __align__(16) unsigned char smem[];
     int *cnt = reinterpret_cast<int *>(smem);  // [T buckets][NW waves]
     int *wsum = cnt + T * NW;                  // [16]
-    const int n = sh.n, E = sh.E, m = sh.m, dv = sh.dv, dc = sh.dc;
+    const int E = sh.E, m = sh.m, dv = sh.dv, dc = sh.dc;
     const bool csr = sh.vsock != nullptr;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t gid = first_graph + blockIdx.x;
@@ -830,35 +1030,9 @@ __global__ __launch_bounds__(T) void sample_regular_kernel(SampleShape sh, uint3
             for (int x = tid; x < E; x += T) chk[x] = buf[x];
         return;
     }
-    for (int x = tid; x < E; x += T) {
-        if (LDSBUF) chk[x] = buf[x];
-        vl[x] = -1;
-    }
-    __threadfence_block();
-    __syncthreads();
-    for (int x = tid; x < E; x += T) {
-        const int v = buf[x];
-        int32_t *row = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
-        const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
-        const int val = csr ? x : x / dc;
-        for (int k = 0; k < deg; ++k)
-            if (atomicCAS(&row[k], -1, val) == -1) break;
-    }
-    __threadfence_block();
-    __syncthreads();
-    for (int v = tid; v < n; v += T) {
-        int32_t *r = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
-        const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
-        for (int x = 1; x < deg; ++x) {
-            const int key = r[x];
-            int y = x - 1;
-            while (y >= 0 && r[y] > key) {
-                r[y + 1] = r[y];
-                --y;
-            }
-            r[y + 1] = key;
-        }
-    }
+    if (LDSBUF)
+        for (int x = tid; x < E; x += T) chk[x] = buf[x];
+    sample_emit_var_side(sh, chk, vl);
 }
 
 // ===========================================================================
@@ -1492,6 +1666,23 @@ static hipError_t launch_sample(const SampleShape &sh, uint64_t seed, uint64_t f
     } while (0)
     if (K == 256 && u16) LDPC_SAMPLE(256, uint16_t, true);
     if (K == 512 && u16) LDPC_SAMPLE(512, uint16_t, true);
+    const int logk1 = big_superbuckets_log2(E);
+    if (u16 && logk1 > 0) {
+        const size_t lds = (size_t)4 * (kBigK2 * 16 + (1 << logk1) * 16 + 16 + 68) + (size_t)4 * kBigCap;
+#define LDPC_BIG(L)                                                                                            \
+    case L: {                                                                                                  \
+        hipError_t e = allow_lds(sample_big_kernel<L>, lds);                                                   \
+        if (e != hipSuccess) return e;                                                                         \
+        hipLaunchKernelGGL(sample_big_kernel<L>, dim3(G), dim3(1024), lds, stream, sh, k0, k1, first_graph,    \
+                           check_lookup, variable_lookup, attempts, max_attempts);                             \
+        return hipGetLastError();                                                                              \
+    }
+        switch (logk1) {
+            LDPC_BIG(1) LDPC_BIG(2) LDPC_BIG(3) LDPC_BIG(4) LDPC_BIG(5) LDPC_BIG(6)
+            default: break;
+        }
+#undef LDPC_BIG
+    }
     LDPC_SAMPLE(1024, int32_t, false);
 #undef LDPC_SAMPLE
 }

@@ -376,7 +376,7 @@ def test_parallel_simulator_per_trial_engine(torch, tmp_path, monkeypatch):
 
 
 # ------------------------------------------------------------ random graphs
-@pytest.mark.parametrize("n,dv,dc", [(1000, 3, 6), (90, 2, 3), (96, 4, 8), (10000, 3, 6), (30000, 3, 6)])
+@pytest.mark.parametrize("n,dv,dc", [(1000, 3, 6), (90, 2, 3), (96, 4, 8), (10000, 3, 6), (30000, 3, 6), (64800, 3, 6)])
 def test_device_sampler_matches_oracle(torch, n, dv, dc):
     from iib_project_ldpc_codes_amd import _native
     L = _native.lib()
