@@ -30,6 +30,26 @@ ITERS = 50
 BATCH = 65536
 SIGMA = 0.85
 HBM_PEAK_GBPS = 8000.0
+# LDS rates per CU per clock by instruction (MI355X_MICROARCH.md, LDS table), 256 CUs at ~2.4 GHz
+LDS_CHIP = 256 * 2.4e9
+LDS_B_PER_CLK = {"ds_read_b64": 256.0, "ds_read_b32": 128.0, "ds_write_b64": 85.0, "ds_write_b32": 64.0}
+
+
+def lds_roofline(n, m, dc, dv, cw_iters_per_s):
+    """The LDS-resident kernel's own bound: every iteration reads and writes each edge message
+    once in the check phase (contiguous, ds_read_b64 / ds_write_b64) and once in the variable
+    phase (gathered, ds_read_b32 / ds_write_b32).  Peak = those bytes at the instruction rates."""
+    chk = m * dc * 4
+    var = n * dv * 4
+    t_peak = (chk / LDS_B_PER_CLK["ds_read_b64"] + chk / LDS_B_PER_CLK["ds_write_b64"]
+              + var / LDS_B_PER_CLK["ds_read_b32"] + var / LDS_B_PER_CLK["ds_write_b32"]) / LDS_CHIP
+    bytes_it = 2 * (chk + var)
+    peak = bytes_it / t_peak / 1e9
+    achieved = bytes_it * cw_iters_per_s / 1e9
+    return {"bound": "lds", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
+            "bytes_per_codeword_iteration": bytes_it,
+            "note": "informational: the unit this kernel is closest to (messages live in LDS); peak = the "
+                    "per-instruction LDS rates of MI355X_MICROARCH.md for this access mix"}
 
 
 def parse():
@@ -138,6 +158,7 @@ def main():
     value = total_cw / elapsed
     b_it = 2 * E * 4 + 2 * g.n * 4
     achieved = b_it * B * ITERS / (kernel_ms * 1e-3) / 1e9
+    kernel_cw_iters = B * ITERS / (kernel_ms * 1e-3)
     traffic = load_traffic()
 
     extras = {}
@@ -208,6 +229,7 @@ def main():
                          "algorithmic_bytes_per_codeword_iteration": b_it,
                          "note": "algorithmic bytes = SURVEY.md 8(d) streaming model; this kernel keeps the "
                                  "messages in LDS, so HBM traffic is ~80 KB/codeword (see DESIGN.md)"},
+            "lds_roofline": lds_roofline(g.n, g.m, DC, DV, kernel_cw_iters),
             "cpu_baseline": cpu,
             "extras": extras,
         }
