@@ -87,3 +87,58 @@ def test_sharded_mc_matches_single_process(world):
     want = oracle_batch_counters(g, 0, rounds * world * B, ITERS)
     for o in out:
         np.testing.assert_array_equal(np.array(o[2]), want)
+
+
+def _worker_ml(rank, world, port, num_tests, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from iib_project_ldpc_codes_amd.graph import TannerGraph
+        from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
+        g = TannerGraph.random_regular(N, 3, 6, seed=5)
+        cptr, cvar, _, _ = g.to_csr()
+        holder = {}
+
+        def executor(first_cw, Bn, stop, counters):  # ML-only batch on the oracle
+            words = oracle.channel(oracle.CH_BEC, EPS, SEED, first_cw, g.n, Bn).astype(np.uint8)
+            _, uns = oracle.ml_decode_batch(cptr, cvar, words, g.n, g.m)
+            c = holder["mc"].counters_ml
+            c[0] += Bn
+            c[1] += int((uns > 0).sum())
+            c[2] += int(uns.sum())
+            c[4] += int(uns.sum())
+
+        mc = MonteCarlo(g, "bec", EPS, ITERS, seed=SEED, batch=B, executor=executor, optimal=True,
+                        message_passing=False)
+        holder["mc"] = mc
+        res = mc.run(num_tests=num_tests, stop_frame_errors=10 ** 9)
+        q.put((rank, res["ml_num_tests"], res["ml_frame_errors"], res["ml_bit_errors"], mc.rounds))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_ml_mc_matches_single_process():
+    """Optimal (ML-only) mode: the ML counters are all-reduced with the others and the
+    trial-count stop uses them (message_passing=False)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    num_tests = 3 * B
+    procs = [ctx.Process(target=_worker_ml, args=(r, world, port, num_tests, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rounds = out[0][4]
+    assert all(o[4] == rounds for o in out) and rounds * world * B >= num_tests
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = TannerGraph.random_regular(N, 3, 6, seed=5)
+    cptr, cvar, _, _ = g.to_csr()
+    T = rounds * world * B
+    words = oracle.channel(oracle.CH_BEC, EPS, SEED, 0, g.n, T).astype(np.uint8)
+    _, uns = oracle.ml_decode_batch(cptr, cvar, words, g.n, g.m)
+    for o in out:
+        assert o[1] == T and o[2] == int((uns > 0).sum()) and o[3] == int(uns.sum())
