@@ -28,6 +28,12 @@ constexpr int kWave = 64;
 #ifndef LDPC_ABLATE_VARW
 #define LDPC_ABLATE_VARW 0
 #endif
+#ifndef LDPC_ABLATE_BARRIER
+#define LDPC_ABLATE_BARRIER 0  // timing ablation only: 1 = drop the two per-iteration barriers (racy)
+#endif
+#ifndef LDPC_ABLATE_PHASE
+#define LDPC_ABLATE_PHASE 0    // timing ablation only: 1 = skip the check phase, 2 = skip the variable phase
+#endif
 #ifndef LDPC_SAMPLER_FIXED_ATT
 #define LDPC_SAMPLER_FIXED_ATT 0  // timing ablation only: exactly this many permutations per graph
 #endif
@@ -457,13 +463,13 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 
         int it = 0;
         for (; it < iters; ++it) {
-            if (it > 0) __syncthreads();  // variable phase (msg, hs) complete
+            if (it > 0 && !LDPC_ABLATE_BARRIER) __syncthreads();  // variable phase (msg, hs) complete
             // check phase; with ET it also evaluates the syndrome of the previous
             // iteration's hard decisions, and the decoder stops before the next
             // variable phase when every check is satisfied
             int unsat = 0;
 #pragma unroll LDPC_CHECK_UNROLL
-            for (int c = tid; c < m; c += T) {
+            for (int c = tid; c < (LDPC_ABLATE_PHASE == 1 ? 0 : m); c += T) {
                 if (ET && it > 0) {
                     int par = 0;
 #pragma unroll
@@ -500,7 +506,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             }
             if constexpr (ET) {
                 if (!__syncthreads_or(unsat | (it == 0))) break;
-            } else {
+            } else if (!LDPC_ABLATE_BARRIER) {
                 __syncthreads();
             }
             // Launder the packed slots so the compiler cannot hoist their
@@ -509,7 +515,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             for (int q = 0; q < (NS + 1) / 2; ++q) asm volatile("" : "+v"(sp[q]));
             // fixed-count decode: the last variable phase runs after the loop
             if (!ET && !MC && it == iters - 1) break;
-            const int errs = var_phase(std::false_type{});
+            const int errs = (LDPC_ABLATE_PHASE == 2) ? 0 : var_phase(std::false_type{});
             if (MC) {
                 const int w = wave_sum(errs);
                 if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[it + 1], w);
