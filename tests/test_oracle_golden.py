@@ -65,3 +65,17 @@ def test_philox_known_answer():
     np.testing.assert_array_equal(
         oracle.philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0]),
         np.array([0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1], np.uint32))
+
+
+def test_oracle_fixed_code_fer_ber_near_reference_probe():
+    """The oracle on the reference-generated n=1000 code, eps=0.4, 50 iterations: FER / BER
+    near the reference C's 9.05e-2 / 2.13e-2 (6,000 trials here, so the
+    tolerance is ~4 sigma of this sample)."""
+    n, k, dv, dc, v2c, c2v = GRAPHS[3]
+    T = 6000
+    words = oracle.channel(oracle.CH_BEC, 0.4, 17, 0, n, T)
+    _, err, _ = oracle.bec_decode_batch(words, 50, v2c, c2v, n, k, dv, dc)
+    final = err[:, -1]
+    fer, ber = float((final > 0).mean()), float(final.sum() / (T * n))
+    assert abs(fer - 0.0905) < 0.015, fer
+    assert abs(ber - 0.0213) < 0.004, ber
