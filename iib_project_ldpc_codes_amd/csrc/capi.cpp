@@ -679,7 +679,8 @@ int ldpc_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_gra
 // Irregular configuration model: degree structure (host arrays) -> device shape buffer
 // [vsock E | cptr m+1 | vptr n+1] on the workspace of `stream` (caller holds g_mu).
 static int csr_shape_upload(int n, int m, const int32_t *var_ptr, const int32_t *check_ptr, Workspace &ws,
-                            int *E_out, const int32_t **vsock, const int32_t **cptr, const int32_t **vptr) {
+                            void *stream, int *E_out, const int32_t **vsock, const int32_t **cptr,
+                            const int32_t **vptr) {
     LDPC_REQUIRE(n > 0 && m > 0 && var_ptr && check_ptr, "bad degree structure");
     LDPC_REQUIRE(var_ptr[0] == 0 && check_ptr[0] == 0, "var_ptr / check_ptr must start at 0");
     for (int v = 0; v < n; ++v) LDPC_REQUIRE(var_ptr[v + 1] >= var_ptr[v], "var_ptr must be non-decreasing");
@@ -691,6 +692,8 @@ static int csr_shape_upload(int n, int m, const int32_t *var_ptr, const int32_t 
         for (int e = var_ptr[v]; e < var_ptr[v + 1]; ++e) h[e] = v;
     std::copy(check_ptr, check_ptr + m + 1, h.begin() + E);
     std::copy(var_ptr, var_ptr + n + 1, h.begin() + E + m + 1);
+    // an earlier sampler launch on this stream may still read the shape buffer
+    LDPC_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
     LDPC_HIP(ws.shape.ensure(h.size() * 4));
     LDPC_HIP(hipMemcpy(ws.shape.p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
     const int32_t *base = static_cast<const int32_t *>(ws.shape.p);
@@ -711,7 +714,7 @@ int ldpc_sample_csr_dev(int n, int m, const int32_t *var_ptr, const int32_t *che
     Workspace &ws = workspace(stream);
     int E = 0;
     const int32_t *vs, *cp, *vp;
-    rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, &E, &vs, &cp, &vp);
+    rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, stream, &E, &vs, &cp, &vp);
     if (rc) return rc;
     LDPC_HIP(launch_sample_csr(n, m, E, vs, cp, vp, seed, first_graph, G, d_check_var, d_var_slot, d_attempts,
                                1 << 20, static_cast<hipStream_t>(stream)));
@@ -727,7 +730,7 @@ int ldpc_sample_csr(int n, int m, const int32_t *var_ptr, const int32_t *check_p
     Workspace &ws = workspace(nullptr);
     int E = 0;
     const int32_t *vs, *cp, *vp;
-    rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, &E, &vs, &cp, &vp);
+    rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, nullptr, &E, &vs, &cp, &vp);
     if (rc) return rc;
     LDPC_HIP(ws.gchk.ensure((size_t)E * G * 4));
     LDPC_HIP(ws.gvar.ensure((size_t)E * G * 4));
