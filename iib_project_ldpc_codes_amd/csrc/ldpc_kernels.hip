@@ -558,6 +558,8 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 //   are kept beside the messages.  Posterior / hard decision are written to
 //   the outputs after every variable phase.
 // ---------------------------------------------------------------------------
+constexpr int kGenDV = 4;  // variable degrees up to this keep their messages in registers
+
 template <int T, int MAXDC, int ALGO, bool ET, bool MC, bool GMEM>
 __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -625,17 +627,37 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
                 __syncthreads();
             }
             int errs = 0;
+            // decisions leave the kernel only when they can be final: the last
+            // fixed-count iteration, or every iteration under early stop
+            const bool out_now = !MC && (ET || it == iters - 1);
             for (int v = tid; v < n; v += T) {
                 const int e0 = a.vptr[v], e1 = a.vptr[v + 1];
                 float s = Ls[v];
-                for (int e = e0; e < e1; ++e) s += MSG(a.vslot[e]);
-                for (int e = e0; e < e1; ++e) {
-                    const int sl = a.vslot[e];
-                    MSG(sl) = s - MSG(sl);
-                    if (ET) hs[sl] = (uint8_t)(s < 0.0f);
+                if (e1 - e0 <= kGenDV) {  // messages and slots read once, kept in registers
+                    int sl[kGenDV];
+                    float cv[kGenDV];
+#pragma unroll
+                    for (int j = 0; j < kGenDV; ++j) {
+                        sl[j] = e0 + j < e1 ? a.vslot[e0 + j] : 0;
+                        cv[j] = e0 + j < e1 ? MSG(sl[j]) : 0.0f;
+                        s += cv[j];
+                    }
+#pragma unroll
+                    for (int j = 0; j < kGenDV; ++j)
+                        if (e0 + j < e1) {
+                            MSG(sl[j]) = s - cv[j];
+                            if (ET) hs[sl[j]] = (uint8_t)(s < 0.0f);
+                        }
+                } else {
+                    for (int e = e0; e < e1; ++e) s += MSG(a.vslot[e]);
+                    for (int e = e0; e < e1; ++e) {
+                        const int sl = a.vslot[e];
+                        MSG(sl) = s - MSG(sl);
+                        if (ET) hs[sl] = (uint8_t)(s < 0.0f);
+                    }
                 }
                 errs += (s < 0.0f);
-                if (!MC) {
+                if (out_now) {
                     if (a.post) a.post[(size_t)b * n + v] = s * Domain<ALGO>::out;
                     if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
                 }
