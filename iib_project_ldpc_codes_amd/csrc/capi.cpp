@@ -193,19 +193,21 @@ hipError_t upload(T **dst, const std::vector<T> &src) {
 // one LDS cycle per distinct address on the busiest bank (bank = slot mod 32).
 // Variables are placed most-constrained first into the first group whose
 // banks for all dv edges are still free, then conflicting ones are moved to
-// conflict-free groups with room.  Padding lanes get dummy slots E + 32 j + f
-// (message value stays 0) on banks the group leaves free.
+// conflict-free groups with room.  Slots are mapped to the kernel's LDS
+// positions first (lds_pair_pos).  Padding lanes get dummy positions S + 32 j + f
+// (S = lds_pair_span) on banks the group leaves free.
 // Measured on a (3,6) n=10000 graph: 3.44 -> ~1.02 cycles per half-wave access
 // at T*VPT = 1.126 n.
 void build_lane_layout(const HostGraph &h, int T, int VPT, std::vector<int32_t> &lane_var,
                        std::vector<int32_t> &lane_slot) {
-    const int n = h.n, dv = h.dv, E = (int)h.cvar.size();
+    const int n = h.n, dv = h.dv, E = lds_pair_span(h.m, h.dc);
     const int P = T * VPT, G = P / 32;
-    std::vector<int> bank((size_t)n * dv);
+    std::vector<int> pos((size_t)n * dv), bank((size_t)n * dv);
     std::vector<int> deg((size_t)dv * 32, 0);
     for (int v = 0; v < n; ++v)
         for (int j = 0; j < dv; ++j) {
-            bank[(size_t)v * dv + j] = h.vslot[(size_t)v * dv + j] & 31;
+            pos[(size_t)v * dv + j] = lds_pair_pos(h.vslot[(size_t)v * dv + j], h.dc);
+            bank[(size_t)v * dv + j] = pos[(size_t)v * dv + j] & 31;
             deg[(size_t)j * 32 + bank[(size_t)v * dv + j]]++;
         }
     std::vector<int> order(n), score(n);
@@ -259,7 +261,7 @@ void build_lane_layout(const HostGraph &h, int T, int VPT, std::vector<int32_t> 
     for (int v = 0; v < n; ++v) {
         const int q = where[v], p = q * 32 + cursor[q]++;
         lane_var[p] = v;
-        for (int j = 0; j < dv; ++j) lane_slot[(size_t)p * dv + j] = h.vslot[(size_t)v * dv + j];
+        for (int j = 0; j < dv; ++j) lane_slot[(size_t)p * dv + j] = pos[(size_t)v * dv + j];
     }
     for (int q = 0; q < G; ++q) {
         std::vector<char> used((size_t)dv * 32, 0);  // [edge j][bank]
@@ -267,7 +269,7 @@ void build_lane_layout(const HostGraph &h, int T, int VPT, std::vector<int32_t> 
             for (int j = 0; j < dv; ++j) used[(size_t)j * 32 + (lane_slot[((size_t)q * 32 + l) * dv + j] & 31)] = 1;
         for (int l = cursor[q]; l < 32; ++l) {
             for (int j = 0; j < dv; ++j) {
-                // dummy slot E + 32 j + f lands on bank (E + f) mod 32: take a free one
+                // dummy position E + 32 j + f lands on bank (E + f) mod 32: take a free one
                 int f = 0;
                 for (int t = 0; t < 32; ++t)
                     if (!used[(size_t)j * 32 + ((E + t) & 31)]) { f = t; break; }
@@ -296,7 +298,7 @@ int device_graph(const HostGraph &h, ldpc_graph **out) {
     if (e == hipSuccess && h.consistent) e = upload(&g->vslot, h.vslot);
     int T = 0, VPT = 0;
     if (e == hipSuccess && h.consistent && h.dv == 3 && h.dc == 6 && lds_shape(h.n, T, VPT) &&
-        (size_t)(h.cvar.size() + kLdsDummy) * 4 <= 150 * 1024) {
+        (size_t)(lds_pair_span(h.m, h.dc) + kLdsDummy) * 4 <= 150 * 1024) {
         std::vector<int32_t> lv, ls;
         build_lane_layout(h, T, VPT, lv, ls);
         e = upload(&g->lane_var, lv);

@@ -27,7 +27,8 @@ struct ldpc_graph {
     // variable; every 32 consecutive positions form one half-wave LDS access.
     int lane_T = 0, lane_VPT = 0;
     int32_t *lane_var = nullptr;   // [T*VPT]    variable id, -1 = padding lane
-    int32_t *lane_slot = nullptr;  // [T*VPT*dv] slot per edge (padding lanes: dummy slots >= E)
+    int32_t *lane_slot = nullptr;  // [T*VPT*dv] LDS position per edge (lds_pair_pos; padding
+                                   //            lanes: dummy positions >= lds_pair_span)
 };
 
 // Threads per workgroup and variables per thread of the LDS-resident kernel
@@ -53,7 +54,19 @@ inline bool lds_shape(int n, int &T, int &VPT) {
         if (1024L * v >= need) { VPT = v; return true; }
     return false;
 }
-constexpr int kLdsDummy = 3 * 32 + 4;  // dummy message slots after the E real ones (DV=3)
+constexpr int kLdsDummy = 3 * 32 + 4;  // dummy message slots after the real ones (DV=3)
+
+// Message positions of the LDS-resident (3,6) kernel.  Checks are paired
+// (2q, 2q+1) and their edges interleaved, [pair q][edge][check of the pair], so
+// one LDS access moves the same edges of both checks and the check update runs
+// on float2 (both checks in every packed VALU op).  With a 2*dc = 12-dword pair
+// stride the check phase's ds_read_b128 / ds_write_b128 are conflict-free.
+inline int lds_pair_pos(int slot, int dc) {
+    const int c = slot / dc, j = slot % dc;
+    return (c >> 1) * 2 * dc + 2 * j + (c & 1);
+}
+// Positions spanned by the m checks (an odd m leaves one phantom check).
+inline int lds_pair_span(int m, int dc) { return ((m + 1) / 2) * 2 * dc; }
 
 namespace ldpc {
 

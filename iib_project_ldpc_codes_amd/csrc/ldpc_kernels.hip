@@ -19,14 +19,8 @@ namespace ldpc {
 namespace {
 
 constexpr int kWave = 64;
-#ifndef LDPC_VAR_GROUP
-#define LDPC_VAR_GROUP 2  // variables per sched_barrier group in the LDS kernel's variable phase
-#endif
 #ifndef LDPC_ABLATE_CHECK
 #define LDPC_ABLATE_CHECK 0
-#endif
-#ifndef LDPC_ABLATE_VARW
-#define LDPC_ABLATE_VARW 0
 #endif
 #ifndef LDPC_ABLATE_BARRIER
 #define LDPC_ABLATE_BARRIER 0  // timing ablation only: 1 = drop the two per-iteration barriers (racy)
@@ -39,9 +33,6 @@ constexpr int kWave = 64;
 #endif
 #ifndef LDPC_SAMPLER_SKIP
 #define LDPC_SAMPLER_SKIP 0       // timing ablation only: 2 = no Fisher-Yates, 8 = no variable_lookup
-#endif
-#ifndef LDPC_CHECK_UNROLL
-#define LDPC_CHECK_UNROLL 2  // two checks in flight per thread (VGPR budget of 4 waves/SIMD)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -271,33 +262,46 @@ template <int ALGO> struct Domain {
     static constexpr float out = ALGO == 0 ? 0.693147180559945309f : 1.0f; // message units -> LLR
 };
 
+// Sum-product check rule in ratio form, shared by all kernels and restated by
+// oracle check_update_spa: for an input message x (log2 units here) e = 2^-min(|x|, 23),
+// a = sign(x) * (1 - e) and b = 2 - |a| (= 1 + e), so tanh(x/2) = a / b; the
+// exclusive products N_j = prod_{i != j} a_i, D_j = prod_{i != j} b_i give the
+// output 2 atanh(N_j / D_j) / ln 2 = log2((D_j + N_j) / (D_j - N_j)).
+//
+// v->c message "on the wire" of the LDS kernel: sum-product sends a itself, so the
+// exponential runs in the variable phase and the check phase only forms
+// b = 2 - |a|; min-sum sends x itself.
+template <int ALGO>
+__device__ __forceinline__ float v2c_wire(float x) {
+    if (ALGO == 0) return copysignf(1.0f - __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x), 0.0f, 23.0f)), x);
+    return x;
+}
+template <int ALGO>
+__device__ __forceinline__ float2 v2c_wire2(float2 x) {
+    if (ALGO == 0) {
+        const float2 e = make_float2(__builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x.x), 0.0f, 23.0f)),
+                                     __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x.y), 0.0f, 23.0f)));
+        const float2 a = make_float2(1.0f, 1.0f) - e;
+        return make_float2(copysignf(a.x, x.x), copysignf(a.y, x.y));
+    }
+    return x;
+}
+
 // Check-node update over D messages in registers; entries i >= d are padding
 // (+inf for min-sum, unit factors for sum-product).  Same product / min order as
 // oracle check_update_{spa,ms}: min-sum is bit-exact with it, sum-product agrees
 // to the stated tolerance.
-// v->c message "on the wire" of the LDS kernel: sum-product sends
-// w = sign(x) * 2^-min(|x|, 23) (the check rule's e_i with the sign of x), so the
-// exponential is evaluated in the LDS-bound variable phase instead of the
-// VALU-bound check phase; min-sum sends x itself.
-template <int ALGO>
-__device__ __forceinline__ float v2c_wire(float x) {
-    if (ALGO == 0) return copysignf(__builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x), 0.0f, 23.0f)), x);
-    return x;
-}
-
 template <int ALGO, int D, bool WIRE = false>
 __device__ __forceinline__ void check_update(float (&x)[D], float alpha, int d = D) {
     if (ALGO == 0) {
-        // (a_i, b_i) pairs live in float2 so 1 -+ e and both product chains are
-        // v_pk_add_f32 / v_pk_mul_f32 (two lanes of work per VALU issue).
+        // (a_i, b_i) pairs live in float2 so both product chains are
+        // v_pk_mul_f32 (two lanes of work per VALU issue).
         float2 ab[D];
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            const float e = WIRE ? fabsf(x[i])
-                                 : __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x[i]), 0.0f, 23.0f));
-            float2 t = make_float2(1.0f, 1.0f) + make_float2(-e, e);
-            t.x = copysignf(t.x, x[i]);
-            ab[i] = i < d ? t : make_float2(1.0f, 1.0f);
+            const float a = WIRE ? x[i]
+                                 : copysignf(1.0f - __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x[i]), 0.0f, 23.0f)), x[i]);
+            ab[i] = i < d ? make_float2(a, 2.0f - fabsf(a)) : make_float2(1.0f, 1.0f);
         }
         float2 pre[D], suf[D];
         pre[0] = make_float2(1.0f, 1.0f);
@@ -329,6 +333,70 @@ __device__ __forceinline__ void check_update(float (&x)[D], float alpha, int d =
     }
 }
 
+// Sum-product update of a PAIR of checks held as float2 lanes (.x = check 2q,
+// .y = check 2q+1; bp_lds_kernel's interleaved layout): the same arithmetic as
+// check_update<0, D, true> per lane, with every product, sum and difference one
+// packed op for both checks.  a[] holds the wire values in and the outputs out.
+// 2 - |x| as one VOP3 op with an abs modifier (the vectoriser would otherwise
+// pack it as v_and + v_pk_add, 1.5 ops per value)
+__device__ __forceinline__ float two_minus_abs(float x) {
+    float r;
+    asm("v_sub_f32_e64 %0, 2.0, |%1|" : "=v"(r) : "v"(x));
+    return r;
+}
+
+template <int D>
+__device__ __forceinline__ void check_update_spa_pair(float2 (&a)[D]) {
+    float2 b[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) b[i] = make_float2(two_minus_abs(a[i].x), two_minus_abs(a[i].y));
+    // prefix products pn[i] = prod_{k<i} a_k (pd: of b), then one running suffix
+    // product walked down from the top: fewer live registers than two arrays
+    float2 pn[D], pd[D];
+    pn[1] = a[0];
+    pd[1] = b[0];
+#pragma unroll
+    for (int i = 2; i < D; ++i) {
+        pn[i] = pn[i - 1] * a[i - 1];
+        pd[i] = pd[i - 1] * b[i - 1];
+    }
+    auto out = [](float2 N, float2 Dd) {
+        const float2 P = Dd + N, Q = Dd - N;
+        const float2 r = P * make_float2(__builtin_amdgcn_rcpf(Q.x), __builtin_amdgcn_rcpf(Q.y));
+        return make_float2(__builtin_amdgcn_logf(r.x), __builtin_amdgcn_logf(r.y));
+    };
+    float2 sn = a[D - 1], sd = b[D - 1];
+    a[D - 1] = out(pn[D - 1], pd[D - 1]);
+#pragma unroll
+    for (int i = D - 2; i >= 1; --i) {
+        const float2 N = pn[i] * sn, Dd = pd[i] * sd;
+        sn = sn * a[i];
+        sd = sd * b[i];
+        a[i] = out(N, Dd);
+    }
+    a[0] = out(sn, sd);
+}
+
+// Byte address (x4) of the low / high 16-bit LDS position packed in p: one SDWA
+// shift instead of an extract and a shift-add.  volatile: re-evaluated every
+// iteration, so the compiler cannot hoist VPT*DV unpacked addresses out of the
+// decode loop (they would not fit the VGPR budget).
+typedef __attribute__((address_space(3))) float lds_f32;  // LDS word at a byte address
+typedef __attribute__((address_space(3))) unsigned char lds_u8;
+
+__device__ __forceinline__ uint32_t pos_lo_x4(uint32_t p) {
+    uint32_t r;
+    asm volatile("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+                 : "=v"(r) : "v"(p));
+    return r;
+}
+__device__ __forceinline__ uint32_t pos_hi_x4(uint32_t p) {
+    uint32_t r;
+    asm volatile("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+                 : "=v"(r) : "v"(p));
+    return r;
+}
+
 struct BpArgs {
     const int32_t *cptr, *cvar, *vptr, *vslot;
     int n, m, E, B;
@@ -351,28 +419,37 @@ struct BpArgs {
 
 // ---------------------------------------------------------------------------
 // 2a. Regular fast path: whole codeword resident in LDS.
-//   LDS  msg[E + dummies] fp32 (check-major slots: check c = [c*DC, c*DC+DC)),
-//        hs[...] u8 hard decision per slot (ET only), curve (MC only).
-//   Thread t owns checks t, t+T, ... and the variables of lane positions
+//   LDS  msg[S + dummies] fp32, S = lds_pair_span(m, DC): check pairs (2q, 2q+1)
+//        interleaved edge by edge ([q][edge][2], lds_pair_pos), hs[...] u8 hard
+//        decision per position (ET only), curve (MC only).
+//   Thread t owns check pairs t, t+T, ... and the variables of lane positions
 //   p = t + i*T (i < VPT) of the host-built conflict-aware layout: every 32
 //   consecutive positions (one half-wave LDS access) hit 32 distinct banks as far
-//   as the graph allows; padding positions address private dummy slots.
-//   Slot indices (packed 2 x 16 bit) and channel LLRs stay in VGPRs for the
-//   whole decode.  Iteration = check phase (contiguous float2 LDS traffic, tanh /
-//   min-sum in registers) | barrier | variable phase (DV gathers, posterior,
-//   extrinsic write-back) | barrier.  Channel LLRs in and posteriors out are
-//   staged through LDS so their HBM traffic stays coalesced.
+//   as the graph allows; padding positions address private dummy positions.
+//   Positions (packed 2 x 16 bit) and channel LLRs stay in VGPRs for the whole
+//   decode.  Iteration = check phase (one conflict-free ds_read_b64 /
+//   ds_write_b64 per edge of a pair; the update runs on float2, both checks in
+//   every packed op) | barrier | variable phase (variables in pairs on float2:
+//   DV gathers, posterior, extrinsic write-back) | barrier.  Channel LLRs in and
+//   posteriors out are staged through LDS so their HBM traffic stays coalesced.
 // ---------------------------------------------------------------------------
 template <int DV, int DC, int T, int VPT, int ALGO, bool ET, bool MC>
 __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
+    static_assert(DC % 2 == 0, "pair layout: the ET parity reads whole words");
     extern __shared__ __align__(16) unsigned char smem[];
     float *msg = reinterpret_cast<float *>(smem);
-    const int Ep = a.E + kLdsDummy;
+    const int Ep = a.E + kLdsDummy;  // a.E = lds_pair_span(m, DC)
     uint8_t *hs = smem + (size_t)Ep * 4;
     int *curve = reinterpret_cast<int *>(smem + (((size_t)Ep * 5 + 15) & ~(size_t)15));
     const int tid = threadIdx.x;
     const int n = a.n, m = a.m, E = a.E, iters = a.max_iters;
-    constexpr int NS = VPT * DV;  // slots reached through my variables
+    const int npairs = (m + 1) >> 1;
+    constexpr int NS = VPT * DV;  // positions reached through my variables
+    // The packed positions carry the dynamic LDS base (in words; not 0 when the
+    // kernel also holds static LDS -- __syncthreads_or reduces through LDS), so
+    // one SDWA shift yields the absolute address of a message.
+    const int lpos0 = (int)((uint32_t)(size_t)(lds_u8 *)smem >> 2);
+    uint8_t *hsb = hs - lpos0;  // hsb[address >> 2] = hs[position]
 
     for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
         const uint64_t cw = a.first_cw + (uint64_t)b;
@@ -400,16 +477,21 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 #pragma unroll
             for (int j = 0; j < DV; ++j) {
                 const int q = i * DV + j;
-                sp[q >> 1] |= (uint32_t)a.lane_slot[p * DV + j] << (16 * (q & 1));
+                sp[q >> 1] |= (uint32_t)(a.lane_slot[p * DV + j] + lpos0) << (16 * (q & 1));
             }
         }
-#define SLOT(i, j) ((int)((sp[((i) * DV + (j)) >> 1] >> (16 * (((i) * DV + (j)) & 1))) & 0xFFFFu))
+        // absolute LDS byte address of my variable i's edge j, and the word there
+        auto addr = [&](int i, int j) -> uint32_t {
+            const int q = i * DV + j;
+            return (q & 1) ? pos_hi_x4(sp[q >> 1]) : pos_lo_x4(sp[q >> 1]);
+        };
+        auto at = [](uint32_t ba) -> lds_f32 & { return *(lds_f32 *)(size_t)ba; };
         __syncthreads();  // staging read before the message initialisation overwrites it
 #pragma unroll
         for (int i = 0; i < VPT; ++i) {
             const float w = v2c_wire<ALGO>(L[i]);
 #pragma unroll
-            for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = w;
+            for (int j = 0; j < DV; ++j) at(addr(i, j)) = w;
         }
         __syncthreads();
         if (MC) {
@@ -427,36 +509,67 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
         auto var_phase = [&](auto final_tag) {
             constexpr bool FINAL = decltype(final_tag)::value;
             int errs = 0;
+            // variables i, i+1 on float2 (packed sums, differences and 1 - e)
 #pragma unroll
-            for (int i = 0; i < VPT; ++i) {
+            for (int i = 0; i + 1 < VPT; i += 2) {
+                uint32_t a0[DV], a1[DV];
+                float2 cv[DV];
+                float2 s = make_float2(L[i], L[i + 1]);
+#pragma unroll
+                for (int j = 0; j < DV; ++j) {  // all addresses first: the gathers issue back to back
+                    a0[j] = addr(i, j);
+                    a1[j] = addr(i + 1, j);
+                }
+#pragma unroll
+                for (int j = 0; j < DV; ++j) cv[j] = make_float2(at(a0[j]), at(a1[j]));
+#pragma unroll
+                for (int j = 0; j < DV; ++j) s = s + cv[j];
+                if constexpr (!FINAL) {
+#pragma unroll
+                    for (int j = 0; j < DV; ++j) {
+                        const float2 w = v2c_wire2<ALGO>(s - cv[j]);
+                        at(a0[j]) = w.x;
+                        at(a1[j]) = w.y;
+                    }
+                }
+                if constexpr (!MC) {
+                    if (FINAL || ET) { pr[i] = s.x; pr[i + 1] = s.y; }
+                }
+                if constexpr (ET) {
+#pragma unroll
+                    for (int j = 0; j < DV; ++j) {
+                        hsb[a0[j] >> 2] = (uint8_t)(s.x < 0.0f);
+                        hsb[a1[j] >> 2] = (uint8_t)(s.y < 0.0f);
+                    }
+                }
+                if constexpr (MC) errs += ((a0[0] < 4u * (E + lpos0)) & (s.x < 0.0f)) + ((a1[0] < 4u * (E + lpos0)) & (s.y < 0.0f));
+                // one pair's gathers in flight per thread (VGPR budget of 4
+                // waves/SIMD; the CU's 16 waves hide LDS latency)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if constexpr (VPT % 2 == 1) {
+                constexpr int i = VPT - 1;
+                uint32_t a0[DV];
                 float cv[DV];
                 float s = L[i];
 #pragma unroll
-                for (int j = 0; j < DV; ++j) {
-                    cv[j] = msg[SLOT(i, j)];
-                    s += cv[j];
-                }
+                for (int j = 0; j < DV; ++j) a0[j] = addr(i, j);
+#pragma unroll
+                for (int j = 0; j < DV; ++j) cv[j] = at(a0[j]);
+#pragma unroll
+                for (int j = 0; j < DV; ++j) s += cv[j];
                 if constexpr (!FINAL) {
-#if LDPC_ABLATE_VARW
 #pragma unroll
-                    for (int j = 0; j < DV; ++j) { float y = s - cv[j]; asm volatile("" :: "v"(y)); }
-#else
-#pragma unroll
-                    for (int j = 0; j < DV; ++j) msg[SLOT(i, j)] = v2c_wire<ALGO>(s - cv[j]);
-#endif
+                    for (int j = 0; j < DV; ++j) at(a0[j]) = v2c_wire<ALGO>(s - cv[j]);
                 }
                 if constexpr (!MC) {
                     if (FINAL || ET) pr[i] = s;
                 }
                 if constexpr (ET) {
 #pragma unroll
-                    for (int j = 0; j < DV; ++j) hs[SLOT(i, j)] = (uint8_t)(s < 0.0f);
+                    for (int j = 0; j < DV; ++j) hsb[a0[j] >> 2] = (uint8_t)(s < 0.0f);
                 }
-                if constexpr (MC) errs += (SLOT(i, 0) < E) & (s < 0.0f);
-                // at most two variables' gathers in flight per thread (VGPR
-                // budget of 4 waves/SIMD; the CU's 16 waves hide LDS latency)
-                if (LDPC_VAR_GROUP > 0 && (i % LDPC_VAR_GROUP) == LDPC_VAR_GROUP - 1)
-                    __builtin_amdgcn_sched_barrier(0);
+                if constexpr (MC) errs += (a0[0] < 4u * (E + lpos0)) & (s < 0.0f);
             }
             return errs;
         };
@@ -468,51 +581,44 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             // iteration's hard decisions, and the decoder stops before the next
             // variable phase when every check is satisfied
             int unsat = 0;
-#pragma unroll LDPC_CHECK_UNROLL
-            for (int c = tid; c < (LDPC_ABLATE_PHASE == 1 ? 0 : m); c += T) {
+            for (int q = tid; q < (LDPC_ABLATE_PHASE == 1 ? 0 : npairs); q += T) {
+                float2 *pp = reinterpret_cast<float2 *>(msg) + q * DC;
                 if (ET && it > 0) {
-                    int par = 0;
+                    // the pair's 2*DC decision bytes: even bytes check 2q, odd 2q+1
+                    const uint32_t *hw = reinterpret_cast<const uint32_t *>(hs + q * 2 * DC);
+                    uint32_t x = 0;
 #pragma unroll
-                    for (int s = 0; s < DC; ++s) par ^= hs[c * DC + s];
-                    unsat |= par;
+                    for (int w = 0; w < DC / 2; ++w) x ^= hw[w];
+                    x ^= x >> 16;
+                    unsat |= (x & 1) | (2 * q + 1 < m ? (x >> 8) & 1 : 0);
                 }
-                float x[DC];
-                if constexpr (DC % 2 == 0) {
-                    const float2 *p = reinterpret_cast<const float2 *>(msg + c * DC);
+                float2 x2[DC];
 #pragma unroll
-                    for (int q = 0; q < DC / 2; ++q) {
-                        const float2 y = p[q];
-                        x[2 * q] = y.x;
-                        x[2 * q + 1] = y.y;
-                    }
-                } else {
-#pragma unroll
-                    for (int s = 0; s < DC; ++s) x[s] = msg[c * DC + s];
-                }
+                for (int i = 0; i < DC; ++i) x2[i] = pp[i];
 #if LDPC_ABLATE_CHECK
 #pragma unroll
-                for (int s = 0; s < DC; ++s) x[s] = x[s] * 0.5f;  // timing ablation only
+                for (int i = 0; i < DC; ++i) x2[i] = x2[i] * make_float2(0.5f, 0.5f);  // timing ablation only
 #else
-                check_update<ALGO, DC, true>(x, a.alpha);
-#endif
-                if constexpr (DC % 2 == 0) {
-                    float2 *p = reinterpret_cast<float2 *>(msg + c * DC);
-#pragma unroll
-                    for (int q = 0; q < DC / 2; ++q) p[q] = make_float2(x[2 * q], x[2 * q + 1]);
+                if constexpr (ALGO == 0) {
+                    check_update_spa_pair<DC>(x2);
                 } else {
+                    float xa[DC], xb[DC];
 #pragma unroll
-                    for (int s = 0; s < DC; ++s) msg[c * DC + s] = x[s];
+                    for (int i = 0; i < DC; ++i) { xa[i] = x2[i].x; xb[i] = x2[i].y; }
+                    check_update<ALGO, DC>(xa, a.alpha);
+                    check_update<ALGO, DC>(xb, a.alpha);
+#pragma unroll
+                    for (int i = 0; i < DC; ++i) x2[i] = make_float2(xa[i], xb[i]);
                 }
+#endif
+#pragma unroll
+                for (int i = 0; i < DC; ++i) pp[i] = x2[i];
             }
             if constexpr (ET) {
                 if (!__syncthreads_or(unsat | (it == 0))) break;
             } else if (!LDPC_ABLATE_BARRIER) {
                 __syncthreads();
             }
-            // Launder the packed slots so the compiler cannot hoist their
-            // unpacking out of the iteration loop (VPT*DV pinned addresses spill).
-#pragma unroll
-            for (int q = 0; q < (NS + 1) / 2; ++q) asm volatile("" : "+v"(sp[q]));
             // fixed-count decode: the last variable phase runs after the loop
             if (!ET && !MC && it == iters - 1) break;
             const int errs = (LDPC_ABLATE_PHASE == 2) ? 0 : var_phase(std::false_type{});
@@ -525,7 +631,6 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             (void)var_phase(std::true_type{});
             it = iters;
         }
-#undef SLOT
         if constexpr (MC) {
             __syncthreads();
             int32_t *tr = a.trial + (size_t)b * (iters + 1);
@@ -1484,7 +1589,7 @@ BecArgs bec_args(const ldpc_graph &g) {
 enum class BpPath { Lds36, Generic8, Generic16, Generic32, GenericG8, GenericG16, GenericG32, None };
 
 size_t lds36_bytes(const ldpc_graph &g, int iters, bool et, bool mc) {
-    const size_t Ep = (size_t)g.E + kLdsDummy;
+    const size_t Ep = (size_t)lds_pair_span(g.m, 6) + kLdsDummy;
     size_t s = Ep * 4;
     if (et || mc) s = (Ep * 5 + 15) & ~(size_t)15;
     if (mc) s += (size_t)(iters + 1) * 4;
@@ -1521,6 +1626,7 @@ hipError_t launch_lds36(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     const size_t lds = lds36_bytes(g, a.max_iters, ET, MC);
     a.lane_var = g.lane_var;
     a.lane_slot = g.lane_slot;
+    a.E = lds_pair_span(g.m, 6);  // message positions (lds_pair_pos), dummies after
 #define LDS36_CASE(TT, VV) \
     if (g.lane_T == TT && g.lane_VPT == VV) return launch_lds36_vpt<VV, TT, ALGO, ET, MC>(g, a, lds, s);
     LDS36_CASE(256, 1) LDS36_CASE(256, 2) LDS36_CASE(256, 3) LDS36_CASE(256, 5) LDS36_CASE(256, 9)

@@ -155,15 +155,18 @@ def test_lane_layout_is_conflict_aware_permutation(n):
     real = lv >= 0
     assert np.array_equal(np.sort(lv[real]), np.arange(n))  # every variable exactly once
     vslot = g.to_csr()[3].reshape(n, 3)
-    np.testing.assert_array_equal(ls[real], vslot[lv[real]])
-    E = g.num_edges
-    assert np.all(ls[~real] >= E)  # padding lanes use private dummy slots
+    # LDS positions (ldpc_internal.hpp lds_pair_pos): check pairs interleaved edge by edge
+    c, j = vslot // 6, vslot % 6
+    pos = (c >> 1) * 12 + 2 * j + (c & 1)
+    np.testing.assert_array_equal(ls[real], pos[lv[real]])
+    span = (g.m + 1) // 2 * 12
+    assert np.all(ls[~real] >= span)  # padding lanes use private dummy positions
     # cost model: LDS cycles per half-wave access = busiest-bank multiplicity
     mult = [np.bincount(ls[q:q + 32, j] % 32, minlength=32).max() for q in range(0, ls.shape[0], 32) for j in range(3)]
     # n = 1000: 28 % spare lanes, nearly conflict-free; n = 10^4: 2.4 % spare (10 variables
     # per thread), where fewer lanes are worth ~1.5 cycles per access
     assert np.mean(mult) < (1.25 if T * V >= 1.1 * n else 1.6), np.mean(mult)
-    base = [np.bincount(vslot[q:q + 32, j] % 32, minlength=32).max() for q in range(0, n - 31, 32) for j in range(3)]
+    base = [np.bincount(pos[q:q + 32, j] % 32, minlength=32).max() for q in range(0, n - 31, 32) for j in range(3)]
     assert np.mean(base) > 2.5  # the naive order would conflict
 
 
