@@ -228,7 +228,10 @@ def main():
                          "traffic": traffic.get("bytes_per_launch") if traffic else None,
                          "algorithmic_bytes_per_codeword_iteration": b_it,
                          "note": "algorithmic bytes = SURVEY.md 8(d) streaming model; this kernel keeps the "
-                                 "messages in LDS, so HBM traffic is ~80 KB/codeword (see DESIGN.md)"},
+                                 "messages in LDS, so its measured HBM traffic is "
+                                 + (f"{traffic['bytes_per_codeword'] / 1e3:.0f} KB" if traffic else "~100 KB")
+                                 + " per codeword (channel LLRs in, posteriors + decisions out), not "
+                                 f"{b_it * ITERS / 1e6:.0f} MB; the kernel is VALU-bound (DESIGN.md 3.1)"},
             "lds_roofline": lds_roofline(g.n, g.m, DC, DV, kernel_cw_iters),
             "cpu_baseline": cpu,
             "extras": extras,

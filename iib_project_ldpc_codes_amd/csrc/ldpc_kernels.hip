@@ -19,6 +19,12 @@ namespace ldpc {
 namespace {
 
 constexpr int kWave = 64;
+#ifndef LDPC_VAR_PAIRS
+#define LDPC_VAR_PAIRS 1  // variable pairs per sched_barrier group in the LDS kernel's variable phase
+#endif
+#ifndef LDPC_CHECK_PAIRS_UNROLL
+#define LDPC_CHECK_PAIRS_UNROLL 1  // check pairs per iteration of the LDS kernel's check loop
+#endif
 #ifndef LDPC_ABLATE_CHECK
 #define LDPC_ABLATE_CHECK 0
 #endif
@@ -543,9 +549,10 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     }
                 }
                 if constexpr (MC) errs += ((a0[0] < 4u * (E + lpos0)) & (s.x < 0.0f)) + ((a1[0] < 4u * (E + lpos0)) & (s.y < 0.0f));
-                // one pair's gathers in flight per thread (VGPR budget of 4
-                // waves/SIMD; the CU's 16 waves hide LDS latency)
-                __builtin_amdgcn_sched_barrier(0);
+                // LDPC_VAR_PAIRS pairs' gathers in flight per thread (VGPR budget of
+                // 4 waves/SIMD; the CU's 16 waves hide LDS latency)
+                if (LDPC_VAR_PAIRS > 0 && (i / 2) % LDPC_VAR_PAIRS == LDPC_VAR_PAIRS - 1)
+                    __builtin_amdgcn_sched_barrier(0);
             }
             if constexpr (VPT % 2 == 1) {
                 constexpr int i = VPT - 1;
@@ -581,6 +588,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             // iteration's hard decisions, and the decoder stops before the next
             // variable phase when every check is satisfied
             int unsat = 0;
+#pragma unroll LDPC_CHECK_PAIRS_UNROLL
             for (int q = tid; q < (LDPC_ABLATE_PHASE == 1 ? 0 : npairs); q += T) {
                 float2 *pp = reinterpret_cast<float2 *>(msg) + q * DC;
                 if (ET && it > 0) {
