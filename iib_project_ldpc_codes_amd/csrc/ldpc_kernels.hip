@@ -272,7 +272,8 @@ template <int ALGO> struct Domain {
 // oracle check_update_spa: for an input message x (log2 units here) e = 2^-min(|x|, 23),
 // a = sign(x) * (1 - e) and b = 2 - |a| (= 1 + e), so tanh(x/2) = a / b; the
 // exclusive products N_j = prod_{i != j} a_i, D_j = prod_{i != j} b_i give the
-// output 2 atanh(N_j / D_j) / ln 2 = log2((D_j + N_j) / (D_j - N_j)).
+// output 2 atanh(N_j / D_j) / ln 2 = log2((D_j + N_j) / (D_j - N_j)), with
+// D_j +- N_j formed as fma(prefix_b_j, suffix_b_j, +-N_j).
 //
 // v->c message "on the wire" of the LDS kernel: sum-product sends a itself, so the
 // exponential runs in the variable phase and the check phase only forms
@@ -318,8 +319,9 @@ __device__ __forceinline__ void check_update(float (&x)[D], float alpha, int d =
         for (int i = D - 2; i >= 0; --i) suf[i] = suf[i + 1] * ab[i + 1];
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            const float2 nd = pre[i] * suf[i];  // (N_i, D_i)
-            x[i] = __builtin_amdgcn_logf((nd.y + nd.x) * __builtin_amdgcn_rcpf(nd.y - nd.x));
+            const float N = pre[i].x * suf[i].x;  // D_i +- N_i fused as in check_update_spa_pair
+            const float P = fmaf(pre[i].y, suf[i].y, N), Q = fmaf(pre[i].y, suf[i].y, -N);
+            x[i] = __builtin_amdgcn_logf(P * __builtin_amdgcn_rcpf(Q));
         }
     } else {
         float m1 = __builtin_inff(), m2 = __builtin_inff();
@@ -351,6 +353,13 @@ __device__ __forceinline__ float two_minus_abs(float x) {
     return r;
 }
 
+// a * b + c per lane as one v_pk_fma_f32 (the SLP vectoriser packs only some)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
+    const f32x2 r = __builtin_elementwise_fma(f32x2{a.x, a.y}, f32x2{b.x, b.y}, f32x2{c.x, c.y});
+    return make_float2(r.x, r.y);
+}
+
 template <int D>
 __device__ __forceinline__ void check_update_spa_pair(float2 (&a)[D]) {
     float2 b[D];
@@ -366,21 +375,25 @@ __device__ __forceinline__ void check_update_spa_pair(float2 (&a)[D]) {
         pn[i] = pn[i - 1] * a[i - 1];
         pd[i] = pd[i - 1] * b[i - 1];
     }
-    auto out = [](float2 N, float2 Dd) {
-        const float2 P = Dd + N, Q = Dd - N;
+    // D_j +- N_j = pd_j * sd_j +- N_j as one fused multiply-add each (oracle: fmaf)
+    auto out = [](float2 N, float2 pdj, float2 sdj) {
+        const float2 P = pk_fma(pdj, sdj, N);
+        const float2 Q = pk_fma(pdj, sdj, make_float2(-N.x, -N.y));
         const float2 r = P * make_float2(__builtin_amdgcn_rcpf(Q.x), __builtin_amdgcn_rcpf(Q.y));
         return make_float2(__builtin_amdgcn_logf(r.x), __builtin_amdgcn_logf(r.y));
     };
+    const float2 one = make_float2(1.0f, 1.0f);
     float2 sn = a[D - 1], sd = b[D - 1];
-    a[D - 1] = out(pn[D - 1], pd[D - 1]);
+    a[D - 1] = out(pn[D - 1], pd[D - 1], one);
 #pragma unroll
     for (int i = D - 2; i >= 1; --i) {
-        const float2 N = pn[i] * sn, Dd = pd[i] * sd;
+        const float2 N = pn[i] * sn;
+        const float2 r = out(N, pd[i], sd);
         sn = sn * a[i];
         sd = sd * b[i];
-        a[i] = out(N, Dd);
+        a[i] = r;
     }
-    a[0] = out(sn, sd);
+    a[0] = out(sn, one, sd);
 }
 
 // Byte address (x4) of the low / high 16-bit LDS position packed in p: one SDWA
