@@ -324,18 +324,22 @@ __device__ __forceinline__ void check_update(float (&x)[D], float alpha, int d =
             x[i] = __builtin_amdgcn_logf(P * __builtin_amdgcn_rcpf(Q));
         }
     } else {
+        // branch-free: m1 = running min, m2 = running second smallest (with
+        // multiplicity) = med3(m1, m2, a); an edge whose magnitude equals m1 gets
+        // m2 (with a tie m2 == m1: the same values as oracle check_update_ms'
+        // "first minimum gets m2")
         float m1 = __builtin_inff(), m2 = __builtin_inff();
-        int i1 = 0, neg = 0;
+        bool neg = false;
 #pragma unroll
         for (int i = 0; i < D; ++i) {
             const float a = fabsf(x[i]);
             neg ^= (x[i] < 0.0f);
-            if (a < m1) { m2 = m1; m1 = a; i1 = i; }
-            else if (a < m2) { m2 = a; }
+            m2 = __builtin_amdgcn_fmed3f(m1, m2, a);
+            m1 = fminf(m1, a);
         }
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            const float mag = alpha * (i == i1 ? m2 : m1);
+            const float mag = alpha * (fabsf(x[i]) == m1 ? m2 : m1);
             x[i] = (neg ^ (x[i] < 0.0f)) ? -mag : mag;
         }
     }
@@ -351,6 +355,29 @@ __device__ __forceinline__ float two_minus_abs(float x) {
     float r;
     asm("v_sub_f32_e64 %0, 2.0, |%1|" : "=v"(r) : "v"(x));
     return r;
+}
+
+// Normalized min-sum update of one degree-6 check, branch-free: the two smallest
+// magnitudes (with multiplicity) from two triples -- m1 = min of the triple minima,
+// m2 = min(max of the triple minima, both triple medians) -- via v_min3 / v_med3.
+// An edge whose magnitude equals m1 gets m2 (with a tie m2 == m1, so this equals
+// oracle check_update_ms' "index of the first minimum gets m2"); signs as there.
+__device__ __forceinline__ void check_update_ms6(float (&x)[6], float alpha) {
+    float ax[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) ax[i] = fabsf(x[i]);
+    const float mn1 = fminf(fminf(ax[0], ax[1]), ax[2]), md1 = __builtin_amdgcn_fmed3f(ax[0], ax[1], ax[2]);
+    const float mn2 = fminf(fminf(ax[3], ax[4]), ax[5]), md2 = __builtin_amdgcn_fmed3f(ax[3], ax[4], ax[5]);
+    const float m1 = fminf(mn1, mn2), m2 = fminf(fminf(fmaxf(mn1, mn2), md1), md2);
+    const float am1 = alpha * m1, am2 = alpha * m2;
+    bool neg = false;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) neg ^= (x[i] < 0.0f);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const float mag = ax[i] == m1 ? am2 : am1;
+        x[i] = (neg ^ (x[i] < 0.0f)) ? -mag : mag;
+    }
 }
 
 // a * b + c per lane as one v_pk_fma_f32 (the SLP vectoriser packs only some)
@@ -626,8 +653,13 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     float xa[DC], xb[DC];
 #pragma unroll
                     for (int i = 0; i < DC; ++i) { xa[i] = x2[i].x; xb[i] = x2[i].y; }
-                    check_update<ALGO, DC>(xa, a.alpha);
-                    check_update<ALGO, DC>(xb, a.alpha);
+                    if constexpr (DC == 6) {
+                        check_update_ms6(xa, a.alpha);
+                        check_update_ms6(xb, a.alpha);
+                    } else {
+                        check_update<ALGO, DC>(xa, a.alpha);
+                        check_update<ALGO, DC>(xb, a.alpha);
+                    }
 #pragma unroll
                     for (int i = 0; i < DC; ++i) x2[i] = make_float2(xa[i], xb[i]);
                 }

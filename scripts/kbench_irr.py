@@ -4,7 +4,7 @@ sys.path.insert(0, os.getcwd())
 import numpy as np, torch
 from iib_project_ldpc_codes_amd import decoder, ensembles
 g = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1)
-B = 8192; it = int(os.environ.get("ITERS", "20"))
+B = 8192; it = int(os.environ.get("ITERS", "20")); algo = int(os.environ.get("ALGO", "0"))
 llr = decoder.channel_dev("awgn", 0.8, 7, 0, g.n, B)
 hard = torch.empty(llr.shape, dtype=torch.uint8, device="cuda")
 s = torch.cuda.current_stream()
@@ -19,6 +19,6 @@ for p in sys.argv[1:]:
     for r in range(3):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(s)
-        assert L.ldpc_bp_decode_batch_dev(h, llr.data_ptr(), B, it, 0, ct.c_float(1.0), 0, None, hard.data_ptr(), None, ct.c_void_p(s.cuda_stream)) == 0
+        assert L.ldpc_bp_decode_batch_dev(h, llr.data_ptr(), B, it, algo, ct.c_float(0.75 if algo else 1.0), 0, None, hard.data_ptr(), None, ct.c_void_p(s.cuda_stream)) == 0
         b.record(s); torch.cuda.synchronize(); ts.append(a.elapsed_time(b))
     print(f"{p:36s} {min(ts):9.2f} ms  {B/min(ts)*1e3*it/100:10.1f} cw/s@100it  errs {int(hard.sum())}")
