@@ -8,7 +8,8 @@ import ctypes as ct
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libldpc_mi355x.so")
+# LDPC_LIB_PATH: benchmark another build of the library (scripts/bench_bec.py --compare)
+LIB_PATH = os.environ.get("LDPC_LIB_PATH") or os.path.join(HERE, "libldpc_mi355x.so")
 
 LDPC_OK = 0
 LDPC_EINVAL, LDPC_ENODEV, LDPC_EHIP, LDPC_ENOMEM, LDPC_EUNSUP = -1, -2, -3, -4, -5

@@ -25,6 +25,9 @@ constexpr int kWave = 64;
 #ifndef LDPC_CHECK_PAIRS_UNROLL
 #define LDPC_CHECK_PAIRS_UNROLL 1  // check pairs per iteration of the LDS kernel's check loop
 #endif
+#ifndef LDPC_BEC_BITS
+#define LDPC_BEC_BITS 1  // fixed-code BEC Monte-Carlo on the bit-sliced kernel when its planes fit LDS
+#endif
 #ifndef LDPC_ABLATE_CHECK
 #define LDPC_ABLATE_CHECK 0
 #endif
@@ -252,6 +255,182 @@ __global__ __launch_bounds__(T) void bec_kernel(BecArgs a) {
         for (int i = tid; i < iters; i += T) e[i] = errs[i];
         if (tid == 0) a.its[b] = it;
     }
+}
+
+// ---------------------------------------------------------------------------
+// 1b. BEC Monte-Carlo, bit-sliced: the same decoder (message_passing.c:7-82 with
+// the all-zero codeword of parallel_simulator.py:222) for 32*W codewords per
+// workgroup at once.  Bit b of word w of variable v is "codeword 32w+b has v
+// erased".  With the all-zero codeword every known bit is 0, so the parity of a
+// check's known bits is 0 and only the erasure planes evolve:
+//   check c:    One[c] = codewords where exactly one of c's slots is erased
+//               (carry-save: two |= one & e; one |= e; One = one & ~two)
+//   variable v: E[v] &= ~OR_{edges e of v, vchk[e] >= 0} One[vchk[e]]
+// which is bec_kernel's rule (an erased variable takes any known check message;
+// known messages are 0) bit for bit, Jacobi (One is built from the old planes).
+// Running every codeword for all iterations in lockstep is exact: a stalled or
+// finished codeword is a fixed point, so its counts repeat (message_passing.c:
+// 16-19 fills errors[it] = errors[it-1]; after the break at a zero count the
+// caller's zeros remain).  Per-codeword counts per iteration come from one LDS
+// atomic per resolved (codeword, variable); its = the first iteration whose
+// count is zero, else iters; the decode stops once no codeword changes.
+// Channel: bit = chan_bec(cw, v) (the stream of bec_kernel / oracle_channel),
+// 32 codewords per half-wave, one Philox block per lane per 4 variables,
+// transposed into the planes by ballots.  Output: trial[b][iters+1] and its[b]
+// in bec_kernel's MC layout, so mc_cutoff / mc_reduce apply unchanged.
+// LDS: E[n][W], One[m][W] (u32), cnt[32W], its[32W], 3 change flags.
+// ---------------------------------------------------------------------------
+template <int W> struct BitsVec;
+template <> struct BitsVec<1> { typedef uint32_t T; };
+template <> struct BitsVec<2> { typedef uint2 T; };
+template <> struct BitsVec<4> { typedef uint4 T; };
+
+template <int W>
+__device__ __forceinline__ void bits_load(const uint32_t *p, uint32_t (&x)[W]) {
+    const typename BitsVec<W>::T v = *reinterpret_cast<const typename BitsVec<W>::T *>(p);
+    if constexpr (W == 1) x[0] = v;
+    if constexpr (W == 2) { x[0] = v.x; x[1] = v.y; }
+    if constexpr (W == 4) { x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w; }
+}
+template <int W>
+__device__ __forceinline__ void bits_store(uint32_t *p, const uint32_t (&x)[W]) {
+    typename BitsVec<W>::T v;
+    if constexpr (W == 1) v = x[0];
+    if constexpr (W == 2) v = make_uint2(x[0], x[1]);
+    if constexpr (W == 4) v = make_uint4(x[0], x[1], x[2], x[3]);
+    *reinterpret_cast<typename BitsVec<W>::T *>(p) = v;
+}
+
+template <int T, int W>
+__global__ __launch_bounds__(T) void bec_mc_bits_kernel(BecArgs a, int B) {
+    static_assert(T % 64 == 0, "half-waves map to 32 codewords");
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int n = a.n, m = a.m, iters = a.max_iters;
+    uint32_t *Ev = reinterpret_cast<uint32_t *>(smem);  // [n][W]
+    uint32_t *On = Ev + (size_t)n * W;                  // [m][W]
+    int *cnt = reinterpret_cast<int *>(On + (size_t)m * W);  // [32W] current erasure count
+    int *itsl = cnt + 32 * W;                                // [32W]
+    uint32_t *flag = reinterpret_cast<uint32_t *>(itsl + 32 * W);  // [3] "some codeword changed"
+    const int NB = 32 * W;
+    const int64_t b0 = (int64_t)blockIdx.x * NB;
+    const int nloc = (int)min((int64_t)NB, (int64_t)B - b0);  // codewords of this block with trial rows
+
+    for (int i = tid; i < NB; i += T) {
+        cnt[i] = 0;
+        itsl[i] = iters;
+    }
+    if (tid < 3) flag[tid] = 0;
+    __syncthreads();
+    // ---- channel: item i = (group g of 4 variables, word w, codeword bit b = i & 31) ----
+    {
+        const int ngr = (n + 3) >> 2;
+        const int bit = tid & 31;
+        int local[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) local[w] = 0;
+        for (int base = tid >> 5; base < ngr * W; base += T >> 5) {
+            const int g = base / W, w = base - g * W;
+            const uint64_t cw = a.first_cw + (uint64_t)(b0 + 32 * w + bit);
+            const uint4 r = philox_block((uint32_t)g, 0u, (uint32_t)cw, (uint32_t)(cw >> 32), a.ch.k0, a.ch.k1);
+            const int hi = (tid & 32);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int v = 4 * g + j;
+                const bool er = v < n && u01(pick4(r, j)) < a.ch.p;
+                const uint64_t bal = __ballot(er);
+                local[w] += er;
+                if (bit == 0 && v < n) Ev[(size_t)v * W + w] = (uint32_t)(hi ? (bal >> 32) : bal);
+            }
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            if (local[w]) atomicAdd(&cnt[32 * w + bit], local[w]);
+    }
+    __syncthreads();
+    for (int i = tid; i < nloc; i += T) a.trial[(size_t)(b0 + i) * (iters + 1)] = cnt[i];
+
+    int it = 0;
+    for (; it < iters; ++it) {
+        // ---- check phase (reads the previous planes only) ----
+        for (int c = tid; c < m; c += T) {
+            const int s0 = a.dc > 0 ? c * a.dc : a.cptr[c];
+            const int s1 = a.dc > 0 ? s0 + a.dc : a.cptr[c + 1];
+            uint32_t one[W], two[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) one[w] = two[w] = 0u;
+            for (int s = s0; s < s1; ++s) {
+                uint32_t e[W];
+                bits_load<W>(Ev + (size_t)a.cvar[s] * W, e);
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    two[w] |= one[w] & e[w];
+                    one[w] |= e[w];
+                }
+            }
+#pragma unroll
+            for (int w = 0; w < W; ++w) one[w] &= ~two[w];
+            bits_store<W>(On + (size_t)c * W, one);
+        }
+        __syncthreads();
+        if (tid == 0) flag[(it + 1) % 3] = 0u;  // next iteration's flag (last read before this barrier)
+        // ---- variable phase ----
+        uint32_t changed = 0u;
+        for (int v = tid; v < n; v += T) {
+            uint32_t e[W], any = 0u;
+            bits_load<W>(Ev + (size_t)v * W, e);
+#pragma unroll
+            for (int w = 0; w < W; ++w) any |= e[w];
+            if (!any) continue;
+            const int e0 = a.dv > 0 ? v * a.dv : a.vptr[v];
+            const int e1 = a.dv > 0 ? e0 + a.dv : a.vptr[v + 1];
+            uint32_t r[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) r[w] = 0u;
+            for (int x = e0; x < e1; ++x) {
+                const int c = a.vchk[x];
+                if (c < 0) continue;
+                uint32_t o[W];
+                bits_load<W>(On + (size_t)c * W, o);
+#pragma unroll
+                for (int w = 0; w < W; ++w) r[w] |= o[w];
+            }
+            uint32_t ne[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                r[w] &= e[w];  // resolved this iteration
+                ne[w] = e[w] & ~r[w];
+                changed |= r[w];
+            }
+            bits_store<W>(Ev + (size_t)v * W, ne);
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                uint32_t q = r[w];
+                while (q) {
+                    const int b = __builtin_ctz(q);
+                    q &= q - 1u;
+                    atomicSub(&cnt[32 * w + b], 1);
+                }
+            }
+        }
+        if (__ballot(changed != 0u) && (tid & (kWave - 1)) == 0) atomicOr(&flag[it % 3], 1u);
+        __syncthreads();
+        for (int i = tid; i < NB; i += T) {
+            const int c = cnt[i];
+            if (c == 0 && itsl[i] == iters) itsl[i] = it;
+            if (i < nloc) a.trial[(size_t)(b0 + i) * (iters + 1) + it + 1] = c;
+        }
+        if (!flag[it % 3]) {  // nothing changed: every codeword is at its fixed point
+            for (int i = tid; i < nloc; i += T) {
+                int32_t *tr = a.trial + (size_t)(b0 + i) * (iters + 1);
+                const int c = cnt[i];
+                for (int j = it + 2; j <= iters; ++j) tr[j] = c;
+            }
+            break;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < nloc; i += T) a.its[b0 + i] = itsl[i];
 }
 
 // ===========================================================================
@@ -1625,6 +1804,33 @@ hipError_t run_bec(const ldpc_graph &g, BecArgs a, int B, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// Bit-sliced BEC Monte-Carlo (bec_mc_bits_kernel): words per variable W and
+// workgroup size for this graph and batch; false when the planes do not fit LDS.
+size_t bec_bits_lds_bytes(const ldpc_graph &g, int W) {
+    return (size_t)(g.n + g.m) * 4 * W + (size_t)256 * W + 16;
+}
+bool bec_bits_shape(const ldpc_graph &g, int B, int &W, int &T) {
+    T = g.n > 4096 ? 512 : 256;
+    for (int w : {4, 2, 1}) {
+        const size_t lds = bec_bits_lds_bytes(g, w);
+        // enough workgroups to fill 256 CUs several times over, LDS for >= 2 per CU
+        if (lds <= 72 * 1024 && ((int64_t)B + 32 * w - 1) / (32 * w) >= 1024) { W = w; return true; }
+    }
+    W = 1;
+    return bec_bits_lds_bytes(g, 1) <= kLdsMax - 4096;
+}
+
+template <int T, int W>
+hipError_t launch_bec_bits(const ldpc_graph &g, const BecArgs &a, int B, hipStream_t stream) {
+    const size_t lds = bec_bits_lds_bytes(g, W);
+    auto k = bec_mc_bits_kernel<T, W>;
+    hipError_t e = allow_lds(k, lds);
+    if (e != hipSuccess) return e;
+    const unsigned grid = (unsigned)(((int64_t)B + 32 * W - 1) / (32 * W));
+    hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, stream, a, B);
+    return hipGetLastError();
+}
+
 BecArgs bec_args(const ldpc_graph &g) {
     BecArgs a{};
     a.cvar = g.cvar;
@@ -1821,6 +2027,17 @@ hipError_t launch_mc_decode(const ldpc_graph &g, int channel, float p, float p2,
         a.first_cw = first_cw;
         a.trial = trial;
         a.its = trial_its;
+        int W = 0, T = 0;
+        if (LDPC_BEC_BITS && bec_bits_shape(g, B, W, T)) {
+            if (T == 256) {
+                if (W == 4) return launch_bec_bits<256, 4>(g, a, B, stream);
+                if (W == 2) return launch_bec_bits<256, 2>(g, a, B, stream);
+                return launch_bec_bits<256, 1>(g, a, B, stream);
+            }
+            if (W == 4) return launch_bec_bits<512, 4>(g, a, B, stream);
+            if (W == 2) return launch_bec_bits<512, 2>(g, a, B, stream);
+            return launch_bec_bits<512, 1>(g, a, B, stream);
+        }
         return run_bec<true>(g, a, B, stream);
     }
     BpArgs a = bp_args(g, B, max_iters, alpha);

@@ -2,7 +2,8 @@
 with the reference's own C (oracle/_ref/message_passing.so, compiled from the
 reference sources) timed on the host as the baseline.
 
-usage: python scripts/bench_bec.py [--cpu-seconds S]
+usage: python scripts/bench_bec.py [--cpu-seconds S] | --mc | --ensemble
+(LDPC_LIB_PATH=<other build>.so times another build of the library)
 Prints one JSON line per workload.
 """
 import argparse
@@ -91,6 +92,30 @@ def main():
                           "cpu_baseline": cpu, "kernel": "bec_kernel"}), flush=True)
 
 
+def mc_fixed(reps=3):
+    """Fixed-code Monte-Carlo (run_simulation_fixed_ldpc's device engine): channel + decode +
+    statistics in one fused batch; bit-sliced kernel where the erasure planes fit LDS."""
+    s = torch.cuda.current_stream()
+    for n, eps, iters, B in ((1000, 0.40, 50, 65536), (1000, 0.40, 50, 262144), (10000, 0.40, 50, 65536),
+                             (64800, 0.40, 200, 4096)):
+        g = TannerGraph.random_regular(n, 3, 6, seed=1)
+        mc = MonteCarlo(g, "bec", eps, iters, seed=9, batch=B)
+        mc.run_batch(0, B)
+        torch.cuda.synchronize()
+        ts = []
+        for r in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            mc.run_batch((r + 1) * B, B)
+            b.record(s)
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b))
+        c = mc.counters.cpu().numpy()
+        print(json.dumps({"workload": f"fixed-code MC (3,6) n={n} eps={eps} {iters} it", "batch": B,
+                          "trials_per_s": B / min(ts) * 1e3, "ms": min(ts),
+                          "fer": float(c[1] / c[0]), "mean_iterations": float(c[3] / c[0])}), flush=True)
+
+
 def ensemble(reps=2):
     """Ensemble mode: a fresh (3,6) graph per trial drawn on the device + decode."""
     s = torch.cuda.current_stream()
@@ -109,6 +134,9 @@ def ensemble(reps=2):
 
 
 if __name__ == "__main__":
+    if "--mc" in sys.argv:
+        mc_fixed()
+        sys.exit(0)
     if "--ensemble" in sys.argv:
         ensemble()
         sys.exit(0)

@@ -327,6 +327,41 @@ def test_mc_bec_sequential_stop_rule(torch):
     np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("n,B,X,stop", [(1000, 65536, -1, 0),      # 2 words per variable
+                                         (1000, 131072, 3, 0),      # 4 words, expurgation
+                                         (1000, 131072, -1, 2000),  # 4 words, exact stop inside a batch
+                                         (6000, 4096, -1, 0)])      # 512-thread workgroups
+def test_mc_bec_bitsliced_shapes_exact(torch, n, B, X, stop):
+    """The bit-sliced BEC Monte-Carlo kernel (32 codewords per word) at every word width and
+    workgroup size it uses, against the oracle's message_passing restatement."""
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = TannerGraph.random_regular(n, 3, 6, seed=23)
+    got = _mc_counters(g, "bec", 0.43, 9, B, 50, X=X, stop=stop)
+    want = _oracle_bec_counters(g, 0.43, 9, B, 50, X=X, stop=stop)
+    if stop:
+        assert want[1] == stop and want[0] < B
+    np.testing.assert_array_equal(got, want)
+
+
+def test_mc_bec_bitsliced_irregular_vs_scalar_kernel(torch):
+    """Irregular CSR graph: bit-sliced MC counters == counters built from the per-codeword
+    BEC kernel (itself pinned to the oracle by test_bec_irregular_csr_vs_oracle)."""
+    from iib_project_ldpc_codes_amd import decoder, ensembles
+    g = ensembles.sample_irregular(ensembles.RSU_DL4, 2000, seed=4)
+    B, iters, eps = 8192, 60, 0.45
+    got = _mc_counters(g, "bec", eps, 31, B, iters)
+    words = oracle.channel(oracle.CH_BEC, eps, 31, 0, g.n, B)
+    _, err, its = decoder.bec_decode(g, words.astype(np.uint8), iters)
+    c = np.zeros(4 + iters + 1, np.int64)
+    curves = np.concatenate([np.count_nonzero(words == 2, axis=1)[:, None], err], axis=1)
+    c[0] = B
+    c[1] = np.count_nonzero(curves[:, -1])
+    c[2] = curves[:, -1].sum()
+    c[3] = its.sum()
+    c[4:] = curves.sum(axis=0)
+    np.testing.assert_array_equal(got, c)
+
+
 def test_mc_minsum_bsc_exact(torch):
     from iib_project_ldpc_codes_amd.graph import TannerGraph
     g = TannerGraph.random_regular(1000, 3, 6, seed=23)
