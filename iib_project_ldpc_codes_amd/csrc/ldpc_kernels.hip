@@ -280,39 +280,43 @@ __global__ __launch_bounds__(T) void bec_kernel(BecArgs a) {
 // in bec_kernel's MC layout, so mc_cutoff / mc_reduce apply unchanged.
 // LDS: E[n][W], One[m][W] (u32), cnt[32W], its[32W], 3 change flags.
 // ---------------------------------------------------------------------------
-template <int W> struct BitsVec;
-template <> struct BitsVec<1> { typedef uint32_t T; };
-template <> struct BitsVec<2> { typedef uint2 T; };
-template <> struct BitsVec<4> { typedef uint4 T; };
+// Plane words: P = uint32_t (32 codewords, W words per variable) or uint8_t (8
+// codewords, W = 1: planes of n + m bytes, for graphs whose u32 planes do not fit).
+template <typename P, int W> struct BitsVec;
+template <> struct BitsVec<uint32_t, 1> { typedef uint32_t T; };
+template <> struct BitsVec<uint32_t, 2> { typedef uint2 T; };
+template <> struct BitsVec<uint32_t, 4> { typedef uint4 T; };
+template <> struct BitsVec<uint8_t, 1> { typedef uint8_t T; };
 
-template <int W>
-__device__ __forceinline__ void bits_load(const uint32_t *p, uint32_t (&x)[W]) {
-    const typename BitsVec<W>::T v = *reinterpret_cast<const typename BitsVec<W>::T *>(p);
+template <typename P, int W>
+__device__ __forceinline__ void bits_load(const P *p, uint32_t (&x)[W]) {
+    const typename BitsVec<P, W>::T v = *reinterpret_cast<const typename BitsVec<P, W>::T *>(p);
     if constexpr (W == 1) x[0] = v;
     if constexpr (W == 2) { x[0] = v.x; x[1] = v.y; }
     if constexpr (W == 4) { x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w; }
 }
-template <int W>
-__device__ __forceinline__ void bits_store(uint32_t *p, const uint32_t (&x)[W]) {
-    typename BitsVec<W>::T v;
-    if constexpr (W == 1) v = x[0];
+template <typename P, int W>
+__device__ __forceinline__ void bits_store(P *p, const uint32_t (&x)[W]) {
+    typename BitsVec<P, W>::T v;
+    if constexpr (W == 1) v = (P)x[0];
     if constexpr (W == 2) v = make_uint2(x[0], x[1]);
     if constexpr (W == 4) v = make_uint4(x[0], x[1], x[2], x[3]);
-    *reinterpret_cast<typename BitsVec<W>::T *>(p) = v;
+    *reinterpret_cast<typename BitsVec<P, W>::T *>(p) = v;
 }
 
-template <int T, int W>
+template <int T, int W, typename P>
 __global__ __launch_bounds__(T) void bec_mc_bits_kernel(BecArgs a, int B) {
-    static_assert(T % 64 == 0, "half-waves map to 32 codewords");
+    static_assert(T % 64 == 0, "lane groups of BITS codewords tile the waves");
+    constexpr int BITS = 8 * sizeof(P);  // codewords per plane word
+    constexpr int NB = BITS * W;         // codewords per workgroup
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x;
     const int n = a.n, m = a.m, iters = a.max_iters;
-    uint32_t *Ev = reinterpret_cast<uint32_t *>(smem);  // [n][W]
-    uint32_t *On = Ev + (size_t)n * W;                  // [m][W]
-    int *cnt = reinterpret_cast<int *>(On + (size_t)m * W);  // [32W] current erasure count
-    int *itsl = cnt + 32 * W;                                // [32W]
-    uint32_t *flag = reinterpret_cast<uint32_t *>(itsl + 32 * W);  // [3] "some codeword changed"
-    const int NB = 32 * W;
+    P *Ev = reinterpret_cast<P *>(smem);  // [n][W]
+    P *On = Ev + (size_t)n * W;           // [m][W]
+    int *cnt = reinterpret_cast<int *>(smem + ((((size_t)n + m) * W * sizeof(P) + 15) & ~(size_t)15));  // [NB]
+    int *itsl = cnt + NB;                                                       // [NB]
+    uint32_t *flag = reinterpret_cast<uint32_t *>(itsl + NB);                   // [3] "some codeword changed"
     const int64_t b0 = (int64_t)blockIdx.x * NB;
     const int nloc = (int)min((int64_t)NB, (int64_t)B - b0);  // codewords of this block with trial rows
 
@@ -322,30 +326,30 @@ __global__ __launch_bounds__(T) void bec_mc_bits_kernel(BecArgs a, int B) {
     }
     if (tid < 3) flag[tid] = 0;
     __syncthreads();
-    // ---- channel: item i = (group g of 4 variables, word w, codeword bit b = i & 31) ----
+    // ---- channel: a group of BITS lanes = one (group g of 4 variables, word w); lane = codeword bit ----
     {
         const int ngr = (n + 3) >> 2;
-        const int bit = tid & 31;
+        const int bit = tid & (BITS - 1);
+        const int shift = (tid & (kWave - 1)) & ~(BITS - 1);  // this group's bits in the wave ballot
         int local[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) local[w] = 0;
-        for (int base = tid >> 5; base < ngr * W; base += T >> 5) {
+        for (int base = tid / BITS; base < ngr * W; base += T / BITS) {
             const int g = base / W, w = base - g * W;
-            const uint64_t cw = a.first_cw + (uint64_t)(b0 + 32 * w + bit);
+            const uint64_t cw = a.first_cw + (uint64_t)(b0 + BITS * w + bit);
             const uint4 r = philox_block((uint32_t)g, 0u, (uint32_t)cw, (uint32_t)(cw >> 32), a.ch.k0, a.ch.k1);
-            const int hi = (tid & 32);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int v = 4 * g + j;
                 const bool er = v < n && u01(pick4(r, j)) < a.ch.p;
                 const uint64_t bal = __ballot(er);
                 local[w] += er;
-                if (bit == 0 && v < n) Ev[(size_t)v * W + w] = (uint32_t)(hi ? (bal >> 32) : bal);
+                if (bit == 0 && v < n) Ev[(size_t)v * W + w] = (P)(bal >> shift);
             }
         }
 #pragma unroll
         for (int w = 0; w < W; ++w)
-            if (local[w]) atomicAdd(&cnt[32 * w + bit], local[w]);
+            if (local[w]) atomicAdd(&cnt[BITS * w + bit], local[w]);
     }
     __syncthreads();
     for (int i = tid; i < nloc; i += T) a.trial[(size_t)(b0 + i) * (iters + 1)] = cnt[i];
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(T) void bec_mc_bits_kernel(BecArgs a, int B) {
             for (int w = 0; w < W; ++w) one[w] = two[w] = 0u;
             for (int s = s0; s < s1; ++s) {
                 uint32_t e[W];
-                bits_load<W>(Ev + (size_t)a.cvar[s] * W, e);
+                bits_load<P, W>(Ev + (size_t)a.cvar[s] * W, e);
 #pragma unroll
                 for (int w = 0; w < W; ++w) {
                     two[w] |= one[w] & e[w];
@@ -370,7 +374,7 @@ __global__ __launch_bounds__(T) void bec_mc_bits_kernel(BecArgs a, int B) {
             }
 #pragma unroll
             for (int w = 0; w < W; ++w) one[w] &= ~two[w];
-            bits_store<W>(On + (size_t)c * W, one);
+            bits_store<P, W>(On + (size_t)c * W, one);
         }
         __syncthreads();
         if (tid == 0) flag[(it + 1) % 3] = 0u;  // next iteration's flag (last read before this barrier)
@@ -378,7 +382,7 @@ __global__ __launch_bounds__(T) void bec_mc_bits_kernel(BecArgs a, int B) {
         uint32_t changed = 0u;
         for (int v = tid; v < n; v += T) {
             uint32_t e[W], any = 0u;
-            bits_load<W>(Ev + (size_t)v * W, e);
+            bits_load<P, W>(Ev + (size_t)v * W, e);
 #pragma unroll
             for (int w = 0; w < W; ++w) any |= e[w];
             if (!any) continue;
@@ -391,7 +395,7 @@ __global__ __launch_bounds__(T) void bec_mc_bits_kernel(BecArgs a, int B) {
                 const int c = a.vchk[x];
                 if (c < 0) continue;
                 uint32_t o[W];
-                bits_load<W>(On + (size_t)c * W, o);
+                bits_load<P, W>(On + (size_t)c * W, o);
 #pragma unroll
                 for (int w = 0; w < W; ++w) r[w] |= o[w];
             }
@@ -402,14 +406,14 @@ __global__ __launch_bounds__(T) void bec_mc_bits_kernel(BecArgs a, int B) {
                 ne[w] = e[w] & ~r[w];
                 changed |= r[w];
             }
-            bits_store<W>(Ev + (size_t)v * W, ne);
+            bits_store<P, W>(Ev + (size_t)v * W, ne);
 #pragma unroll
             for (int w = 0; w < W; ++w) {
                 uint32_t q = r[w];
                 while (q) {
                     const int b = __builtin_ctz(q);
                     q &= q - 1u;
-                    atomicSub(&cnt[32 * w + b], 1);
+                    atomicSub(&cnt[BITS * w + b], 1);
                 }
             }
         }
@@ -1804,29 +1808,38 @@ hipError_t run_bec(const ldpc_graph &g, BecArgs a, int B, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// Bit-sliced BEC Monte-Carlo (bec_mc_bits_kernel): words per variable W and
-// workgroup size for this graph and batch; false when the planes do not fit LDS.
-size_t bec_bits_lds_bytes(const ldpc_graph &g, int W) {
-    return (size_t)(g.n + g.m) * 4 * W + (size_t)256 * W + 16;
+// Bit-sliced BEC Monte-Carlo (bec_mc_bits_kernel): plane word (u32 x W words per
+// variable, or u8 = 8 codewords for graphs whose u32 planes do not fit) and
+// workgroup size for this graph and batch; false when not even u8 planes fit.
+size_t bec_bits_lds_bytes(const ldpc_graph &g, int W, int bytes_per_word) {
+    const int NB = 8 * bytes_per_word * W;
+    return ((((size_t)g.n + g.m) * W * bytes_per_word + 15) & ~(size_t)15) + (size_t)8 * NB + 16;
 }
-bool bec_bits_shape(const ldpc_graph &g, int B, int &W, int &T) {
+bool bec_bits_shape(const ldpc_graph &g, int B, int &W, int &T, int &bytes) {
     T = g.n > 4096 ? 512 : 256;
+    bytes = 4;
     for (int w : {4, 2, 1}) {
-        const size_t lds = bec_bits_lds_bytes(g, w);
         // enough workgroups to fill 256 CUs several times over, LDS for >= 2 per CU
-        if (lds <= 72 * 1024 && ((int64_t)B + 32 * w - 1) / (32 * w) >= 1024) { W = w; return true; }
+        if (bec_bits_lds_bytes(g, w, 4) <= 72 * 1024 && ((int64_t)B + 32 * w - 1) / (32 * w) >= 1024) {
+            W = w;
+            return true;
+        }
     }
     W = 1;
-    return bec_bits_lds_bytes(g, 1) <= kLdsMax - 4096;
+    if (bec_bits_lds_bytes(g, 1, 4) <= kLdsMax - 4096) return true;
+    T = 1024;
+    bytes = 1;
+    return bec_bits_lds_bytes(g, 1, 1) <= kLdsMax - 4096;
 }
 
-template <int T, int W>
+template <int T, int W, typename P>
 hipError_t launch_bec_bits(const ldpc_graph &g, const BecArgs &a, int B, hipStream_t stream) {
-    const size_t lds = bec_bits_lds_bytes(g, W);
-    auto k = bec_mc_bits_kernel<T, W>;
+    const size_t lds = bec_bits_lds_bytes(g, W, (int)sizeof(P));
+    auto k = bec_mc_bits_kernel<T, W, P>;
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
-    const unsigned grid = (unsigned)(((int64_t)B + 32 * W - 1) / (32 * W));
+    constexpr int NB = 8 * (int)sizeof(P) * W;
+    const unsigned grid = (unsigned)(((int64_t)B + NB - 1) / NB);
     hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, stream, a, B);
     return hipGetLastError();
 }
@@ -2027,16 +2040,17 @@ hipError_t launch_mc_decode(const ldpc_graph &g, int channel, float p, float p2,
         a.first_cw = first_cw;
         a.trial = trial;
         a.its = trial_its;
-        int W = 0, T = 0;
-        if (LDPC_BEC_BITS && bec_bits_shape(g, B, W, T)) {
+        int W = 0, T = 0, bytes = 0;
+        if (LDPC_BEC_BITS && bec_bits_shape(g, B, W, T, bytes)) {
+            if (bytes == 1) return launch_bec_bits<1024, 1, uint8_t>(g, a, B, stream);
             if (T == 256) {
-                if (W == 4) return launch_bec_bits<256, 4>(g, a, B, stream);
-                if (W == 2) return launch_bec_bits<256, 2>(g, a, B, stream);
-                return launch_bec_bits<256, 1>(g, a, B, stream);
+                if (W == 4) return launch_bec_bits<256, 4, uint32_t>(g, a, B, stream);
+                if (W == 2) return launch_bec_bits<256, 2, uint32_t>(g, a, B, stream);
+                return launch_bec_bits<256, 1, uint32_t>(g, a, B, stream);
             }
-            if (W == 4) return launch_bec_bits<512, 4>(g, a, B, stream);
-            if (W == 2) return launch_bec_bits<512, 2>(g, a, B, stream);
-            return launch_bec_bits<512, 1>(g, a, B, stream);
+            if (W == 4) return launch_bec_bits<512, 4, uint32_t>(g, a, B, stream);
+            if (W == 2) return launch_bec_bits<512, 2, uint32_t>(g, a, B, stream);
+            return launch_bec_bits<512, 1, uint32_t>(g, a, B, stream);
         }
         return run_bec<true>(g, a, B, stream);
     }

@@ -330,7 +330,8 @@ def test_mc_bec_sequential_stop_rule(torch):
 @pytest.mark.parametrize("n,B,X,stop", [(1000, 65536, -1, 0),      # 2 words per variable
                                          (1000, 131072, 3, 0),      # 4 words, expurgation
                                          (1000, 131072, -1, 2000),  # 4 words, exact stop inside a batch
-                                         (6000, 4096, -1, 0)])      # 512-thread workgroups
+                                         (6000, 4096, -1, 0),       # 512-thread workgroups
+                                         (64800, 512, 3, 0)])       # byte planes (8 codewords)
 def test_mc_bec_bitsliced_shapes_exact(torch, n, B, X, stop):
     """The bit-sliced BEC Monte-Carlo kernel (32 codewords per word) at every word width and
     workgroup size it uses, against the oracle's message_passing restatement."""
