@@ -181,6 +181,22 @@ def main():
         b.record(stream)
         torch.cuda.synchronize()
         extras["minsum_50it_codewords_per_s"] = B / (a.elapsed_time(b) * 1e-3)
+        # BEC Monte-Carlo on a fixed code (channel + decode + counters, bit-sliced kernel): the
+        # device engine of run_simulation_fixed_ldpc at the configs[0] / configs[4] shapes
+        from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
+        for key, n_b, eps, its_b, Bb in (("bec_mc_cfg1_n1000_eps0.4_50it", 1000, 0.40, 50, 262144),
+                                         ("bec_mc_cfg5_n64800_eps0.4_200it", 64800, 0.40, 200, 4096)):
+            gb = TannerGraph.random_regular(n_b, DV, DC, seed=1)
+            mc = MonteCarlo(gb, "bec", eps, its_b, seed=9, batch=Bb)
+            mc.run_batch(0, Bb)
+            torch.cuda.synchronize()
+            a.record(stream)
+            mc.run_batch(Bb, Bb)
+            b.record(stream)
+            torch.cuda.synchronize()
+            cnt = mc.counters.cpu().numpy()
+            extras[key] = {"trials_per_s": Bb / (a.elapsed_time(b) * 1e-3), "batch": Bb,
+                           "fer": float(cnt[1] / cnt[0]), "mean_iterations": float(cnt[3] / cnt[0])}
         # BEC erasure decoding (message_passing.c semantics, bit-exact): configs[0] and configs[4] shapes
         for key, n_b, eps, its_b, Bb in (("bec_cfg1_n1000_eps0.4_50it", 1000, 0.40, 50, 65536),
                                          ("bec_cfg5_n64800_eps0.4_200it", 64800, 0.40, 200, 4096)):
