@@ -16,6 +16,10 @@
 #include <vector>
 
 #include "ldpc_internal.hpp"
+
+#ifndef LDPC_IRR
+#define LDPC_IRR 1  // irregular graphs on bp_irr_kernel when in range
+#endif
 #include "ldpc_mi355x.h"
 
 namespace ldpc {
@@ -263,6 +267,11 @@ void build_lane_layout(const HostGraph &h, int T, int VPT, std::vector<int32_t> 
         lane_var[p] = v;
         for (int j = 0; j < dv; ++j) lane_slot[(size_t)p * dv + j] = pos[(size_t)v * dv + j];
     }
+#if LDPC_ABLATE_LAYOUT  // timing ablation only (wrong results): conflict-free fake positions
+    for (int p = 0; p < P; ++p)
+        for (int j = 0; j < dv; ++j) lane_slot[(size_t)p * dv + j] = (p * dv + j) % E;
+    return;
+#endif
     for (int q = 0; q < G; ++q) {
         std::vector<char> used((size_t)dv * 32, 0);  // [edge j][bank]
         for (int l = 0; l < cursor[q]; ++l)
@@ -278,6 +287,79 @@ void build_lane_layout(const HostGraph &h, int T, int VPT, std::vector<int32_t> 
             }
         }
     }
+}
+
+// Layout of the irregular kernel (bp_irr_kernel, ldpc_internal.hpp): rows of
+// 1024 checks, DC = 6 or 8 slots per check (absent slots hold the check rule's
+// neutral value), positions k-major so a row's slots are lane-contiguous (LDS
+// conflict-free / coalesced in the slab) and whole rows are either in LDS or in
+// the slab; variables sorted by degree, every degree class padded to whole
+// 64-lane rows so the degree is wave-uniform; padding lanes of a class get
+// private dummy positions after the checks'.  Returns false when the graph is
+// outside the kernel's range (variable degree > 4, check degree > 8, > 16 rows,
+// > 20 variables per thread, positions beyond 16 bits).
+bool build_irr_layout(const HostGraph &h, int &VPT, int &KC, int &DC, int &S, int &P,
+                      std::vector<int32_t> &lane, std::vector<int32_t> &cdeg) {
+    const int T = kIrrT, n = h.n, m = h.m;
+    if (h.max_vdeg > 4 || h.max_cdeg > 8 || n <= 0 || m <= 0) return false;
+    DC = h.max_cdeg <= 6 ? 6 : 8;
+    KC = (m + T - 1) / T;
+    if (KC > 16) return false;
+    const int PC = KC * DC * T;  // check positions
+    std::vector<int> slot_check(h.cvar.size());
+    for (int c = 0; c < m; ++c)
+        for (int x = h.cptr[c]; x < h.cptr[c + 1]; ++x) slot_check[x] = c;
+    auto pos_of = [&](int slot) {
+        const int c = slot_check[slot], j = slot - h.cptr[c];
+        return ((c / T) * DC + j) * T + (c % T);
+    };
+    std::vector<int> order(n);
+    for (int v = 0; v < n; ++v) order[v] = v;
+    auto deg = [&](int v) { return h.vptr[v + 1] - h.vptr[v]; };
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return deg(x) > deg(y); });
+    // lanes: degree classes padded to 64
+    std::vector<int> lv;  // var id per lane, -(d+1) for a padding lane of degree d
+    for (size_t a = 0; a < order.size();) {
+        const int d = deg(order[a]);
+        size_t b = a;
+        while (b < order.size() && deg(order[b]) == d) lv.push_back(order[b++]);
+        while (lv.size() % 64) lv.push_back(-(d + 1));
+        a = b;
+    }
+    const int need = (int)((lv.size() + T - 1) / T);
+    VPT = 0;
+    for (int v : {1, 2, 5, 10, 20})
+        if (v >= need) { VPT = v; break; }
+    if (!VPT) return false;
+    const int L = T * VPT;
+    lane.assign((size_t)3 * L, 0);
+    int dummy = PC;
+    for (int q = 0; q < L; ++q) {
+        int p4[4] = {0xFFFF, 0xFFFF, 0xFFFF, 0xFFFF};
+        int var = -1;
+        if (q < (int)lv.size() && lv[q] >= 0) {
+            var = lv[q];
+            for (int j = 0; j < deg(var); ++j) p4[j] = pos_of(h.vslot[h.vptr[var] + j]);
+        } else if (q < (int)lv.size()) {
+            for (int j = 0; j < -lv[q] - 1; ++j) p4[j] = dummy++;
+        }
+        lane[q] = var;
+        lane[(size_t)L + q] = p4[0] | (p4[1] << 16);
+        lane[(size_t)2 * L + q] = p4[2] | (p4[3] << 16);
+    }
+    P = dummy;
+    if (P >= 0xFFFF) return false;
+    // whole rows in LDS while they fit (the dummies too when everything fits)
+    const int rows_lds = (int)std::min<size_t>((size_t)KC, kIrrLdsMsgBytes / ((size_t)DC * T * 4));
+    S = rows_lds == KC && (size_t)P * 4 <= kIrrLdsMsgBytes ? P : rows_lds * DC * T;
+    cdeg.assign((size_t)2 * T, 0);
+    for (int t = 0; t < T; ++t)
+        for (int k = 0; k < KC; ++k) {
+            const int c = k * T + t;
+            const int d = c < m ? h.cptr[c + 1] - h.cptr[c] : 0;
+            cdeg[(size_t)(k >> 3) * T + t] |= d << (4 * (k & 7));
+        }
+    return true;
 }
 
 int device_graph(const HostGraph &h, ldpc_graph **out) {
@@ -305,6 +387,15 @@ int device_graph(const HostGraph &h, ldpc_graph **out) {
         if (e == hipSuccess) e = upload(&g->lane_slot, ls);
         g->lane_T = T;
         g->lane_VPT = VPT;
+    }
+    if (e == hipSuccess && h.consistent && !g->lane_var && LDPC_IRR) {
+        std::vector<int32_t> ln, cd;
+        int VPT_ = 0, KC = 0, DC = 0, S = 0, P = 0;
+        if (build_irr_layout(h, VPT_, KC, DC, S, P, ln, cd)) {
+            e = upload(&g->irr_lane, ln);
+            if (e == hipSuccess) e = upload(&g->irr_cdeg, cd);
+            g->irr_VPT = VPT_; g->irr_KC = KC; g->irr_DC = DC; g->irr_S = S; g->irr_P = P;
+        }
     }
     if (e != hipSuccess) {
         set_error(std::string("graph upload: ") + hipGetErrorString(e));
@@ -382,6 +473,8 @@ void ldpc_graph_destroy(ldpc_graph *g) {
     (void)hipFree(g->vslot);
     (void)hipFree(g->lane_var);
     (void)hipFree(g->lane_slot);
+    (void)hipFree(g->irr_lane);
+    (void)hipFree(g->irr_cdeg);
     delete g;
 }
 

@@ -29,7 +29,20 @@ struct ldpc_graph {
     int32_t *lane_var = nullptr;   // [T*VPT]    variable id, -1 = padding lane
     int32_t *lane_slot = nullptr;  // [T*VPT*dv] LDS position per edge (lds_pair_pos; padding
                                    //            lanes: dummy positions >= lds_pair_span)
+    // Layout of the irregular kernel (bp_irr_kernel; build_irr_layout in capi.cpp):
+    // check c = k*1024 + t (thread t, row k < irr_KC), its slot j at position
+    // (k*irr_DC + j)*1024 + t; positions [0, irr_S) live in LDS, [irr_S, irr_P) in a
+    // per-workgroup global slab.  Lane p = i*1024 + t is thread t's i-th variable.
+    int irr_VPT = 0, irr_KC = 0, irr_DC = 0, irr_S = 0, irr_P = 0;
+    int32_t *irr_lane = nullptr;  // [3][1024*VPT]: variable id (-1 pad), positions j0|j1<<16, j2|j3<<16
+                                  // (0xFFFF = no edge; lanes of one 64-lane row share a degree)
+    int32_t *irr_cdeg = nullptr;  // [2][1024]: degrees of thread t's checks, 4 bits per row k
 };
+
+// Irregular kernel (bp_irr_kernel): 1024 threads; LDS room for messages (bytes)
+// after the early-stop syndrome bits and the Monte-Carlo curve.
+constexpr int kIrrT = 1024;
+constexpr size_t kIrrLdsMsgBytes = 148 * 1024;
 
 // Threads per workgroup and variables per thread of the LDS-resident kernel
 // for block length n: >= 2 % spare lanes for the conflict-aware layout.  (At

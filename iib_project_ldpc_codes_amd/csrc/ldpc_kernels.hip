@@ -644,6 +644,9 @@ struct BpArgs {
     // LDS kernel lane layout (ldpc_graph::lane_var / lane_slot)
     const int32_t *lane_var, *lane_slot;
     int lds_slots;  // generic GMEM kernel: message slots [0, lds_slots) kept in LDS
+    // irregular kernel layout (ldpc_graph::irr_*)
+    const int32_t *irr_lane, *irr_cdeg;
+    int irr_KC, irr_S, irr_P;
 };
 
 // ---------------------------------------------------------------------------
@@ -900,6 +903,12 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 //   the outputs after every variable phase.
 // ---------------------------------------------------------------------------
 constexpr int kGenDV = 4;  // variable degrees up to this keep their messages in registers
+#ifndef LDPC_GEN_UC
+#define LDPC_GEN_UC 2  // checks per step of the generic kernel's check phase (loads batched)
+#endif
+#ifndef LDPC_GEN_UV
+#define LDPC_GEN_UV 4  // variables per step of the generic kernel's variable phase
+#endif
 
 template <int T, int MAXDC, int ALGO, bool ET, bool MC, bool GMEM>
 __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
@@ -916,8 +925,22 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
     // GMEM: the first S message slots live in LDS, the rest in the L2-resident
     // global slab (generic pointers -> flat loads pick the space per lane).
     const int S = GMEM ? a.lds_slots : 0;
-    float *msg_lds = reinterpret_cast<float *>(smem + (MC ? (((size_t)(iters + 1) * 4 + 15) & ~(size_t)15) : 0));
-    auto MSG = [&](int e) -> float & { return (GMEM && e < S) ? msg_lds[e] : msg_all[e]; };
+    // explicit address spaces (no generic pointer selects: a select between an LDS
+    // and a global pointer trips the gfx950 backend once the loops are unrolled)
+    lds_f32 *msg_lds = (lds_f32 *)((lds_u8 *)smem + (MC ? (((size_t)(iters + 1) * 4 + 15) & ~(size_t)15) : 0));
+    lds_f32 *msg_l = (lds_f32 *)(lds_u8 *)smem;  // !GMEM: every message in LDS
+    auto LD = [&](int e) -> float {
+        if constexpr (GMEM) return e < S ? msg_lds[e] : msg_all[e];
+        else return msg_l[e];
+    };
+    auto ST = [&](int e, float x) {
+        if constexpr (GMEM) {
+            if (e < S) msg_lds[e] = x;
+            else msg_all[e] = x;
+        } else {
+            msg_l[e] = x;
+        }
+    };
 
     for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
         const uint64_t cw = a.first_cw + (uint64_t)b;
@@ -932,7 +955,7 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
             const float l2 = l * Domain<ALGO>::in;
             Ls[v] = l2;
             err0 += (l < 0.0f);
-            for (int e = a.vptr[v]; e < a.vptr[v + 1]; ++e) MSG(a.vslot[e]) = l2;
+            for (int e = a.vptr[v]; e < a.vptr[v + 1]; ++e) ST(a.vslot[e], l2);
             if (!MC) {
                 if (a.post) a.post[(size_t)b * n + v] = l;
                 if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(l < 0.0f);
@@ -947,20 +970,36 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
         for (; it < iters; ++it) {
             if (it > 0) __syncthreads();  // variable phase (messages, hs) complete
             int unsat = 0;                // ET: syndrome of the previous hard decisions
-            for (int c = tid; c < m; c += T) {
-                const int s0 = a.cptr[c], d = a.cptr[c + 1] - s0;
-                if (ET && it > 0) {
-                    int par = 0;
-                    for (int s = 0; s < d; ++s) par ^= hs[s0 + s];
-                    unsat |= par;
+            // LDPC_GEN_UC checks per step: every load of the step is issued before
+            // the first use, so the L2 latency of the CSR and slab reads overlaps
+            for (int c0 = tid; c0 < m; c0 += T * LDPC_GEN_UC) {
+                int s0[LDPC_GEN_UC], d[LDPC_GEN_UC];
+#pragma unroll
+                for (int u = 0; u < LDPC_GEN_UC; ++u) {
+                    const int c = c0 + u * T, cc = c < m ? c : m - 1;
+                    s0[u] = a.cptr[cc];
+                    d[u] = c < m ? a.cptr[cc + 1] - s0[u] : 0;
                 }
-                float x[MAXDC];
+                if (ET && it > 0) {
 #pragma unroll
-                for (int s = 0; s < MAXDC; ++s) x[s] = s < d ? MSG(s0 + s) : __builtin_inff();
-                check_update<ALGO, MAXDC>(x, a.alpha, d);
+                    for (int u = 0; u < LDPC_GEN_UC; ++u) {
+                        int par = 0;
+                        for (int q = 0; q < d[u]; ++q) par ^= hs[s0[u] + q];
+                        unsat |= par;
+                    }
+                }
+                float x[LDPC_GEN_UC][MAXDC];
 #pragma unroll
-                for (int s = 0; s < MAXDC; ++s)
-                    if (s < d) MSG(s0 + s) = x[s];
+                for (int u = 0; u < LDPC_GEN_UC; ++u)
+#pragma unroll
+                    for (int q = 0; q < MAXDC; ++q) x[u][q] = q < d[u] ? LD(s0[u] + q) : __builtin_inff();
+#pragma unroll
+                for (int u = 0; u < LDPC_GEN_UC; ++u) {
+                    check_update<ALGO, MAXDC>(x[u], a.alpha, d[u]);
+#pragma unroll
+                    for (int q = 0; q < MAXDC; ++q)
+                        if (q < d[u]) ST(s0[u] + q, x[u][q]);
+                }
             }
             if constexpr (ET) {
                 if (!__syncthreads_or(unsat | (it == 0))) break;
@@ -971,36 +1010,55 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
             // decisions leave the kernel only when they can be final: the last
             // fixed-count iteration, or every iteration under early stop
             const bool out_now = !MC && (ET || it == iters - 1);
-            for (int v = tid; v < n; v += T) {
-                const int e0 = a.vptr[v], e1 = a.vptr[v + 1];
-                float s = Ls[v];
-                if (e1 - e0 <= kGenDV) {  // messages and slots read once, kept in registers
-                    int sl[kGenDV];
-                    float cv[kGenDV];
+            // LDPC_GEN_UV variables per step, loads batched as in the check phase
+            for (int v0 = tid; v0 < n; v0 += T * LDPC_GEN_UV) {
+                int e0[LDPC_GEN_UV], dg[LDPC_GEN_UV];
+                float sv[LDPC_GEN_UV];
 #pragma unroll
-                    for (int j = 0; j < kGenDV; ++j) {
-                        sl[j] = e0 + j < e1 ? a.vslot[e0 + j] : 0;
-                        cv[j] = e0 + j < e1 ? MSG(sl[j]) : 0.0f;
-                        s += cv[j];
-                    }
-#pragma unroll
-                    for (int j = 0; j < kGenDV; ++j)
-                        if (e0 + j < e1) {
-                            MSG(sl[j]) = s - cv[j];
-                            if (ET) hs[sl[j]] = (uint8_t)(s < 0.0f);
-                        }
-                } else {
-                    for (int e = e0; e < e1; ++e) s += MSG(a.vslot[e]);
-                    for (int e = e0; e < e1; ++e) {
-                        const int sl = a.vslot[e];
-                        MSG(sl) = s - MSG(sl);
-                        if (ET) hs[sl] = (uint8_t)(s < 0.0f);
-                    }
+                for (int u = 0; u < LDPC_GEN_UV; ++u) {
+                    const int v = v0 + u * T, vc = v < n ? v : n - 1;  // clamped: loads stay unconditional
+                    e0[u] = a.vptr[vc];
+                    dg[u] = v < n ? a.vptr[vc + 1] - e0[u] : 0;
+                    sv[u] = Ls[vc];
                 }
-                errs += (s < 0.0f);
-                if (out_now) {
-                    if (a.post) a.post[(size_t)b * n + v] = s * Domain<ALGO>::out;
-                    if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
+                int sl[LDPC_GEN_UV][kGenDV];
+                float cv[LDPC_GEN_UV][kGenDV];
+#pragma unroll
+                for (int u = 0; u < LDPC_GEN_UV; ++u)
+#pragma unroll
+                    for (int j = 0; j < kGenDV; ++j) sl[u][j] = j < dg[u] ? a.vslot[e0[u] + j] : 0;
+#pragma unroll
+                for (int u = 0; u < LDPC_GEN_UV; ++u)
+#pragma unroll
+                    for (int j = 0; j < kGenDV; ++j) cv[u][j] = j < dg[u] ? LD(sl[u][j]) : 0.0f;
+#pragma unroll
+                for (int u = 0; u < LDPC_GEN_UV; ++u) {
+                    const int v = v0 + u * T;
+                    if (v >= n) continue;
+                    float s = sv[u];
+                    if (dg[u] <= kGenDV) {  // messages and slots read once, kept in registers
+#pragma unroll
+                        for (int j = 0; j < kGenDV; ++j) s += cv[u][j];  // absent edges add +0
+#pragma unroll
+                        for (int j = 0; j < kGenDV; ++j)
+                            if (j < dg[u]) {
+                                ST(sl[u][j], s - cv[u][j]);
+                                if (ET) hs[sl[u][j]] = (uint8_t)(s < 0.0f);
+                            }
+                    } else {
+                        const int e1 = e0[u] + dg[u];
+                        for (int e = e0[u]; e < e1; ++e) s += LD(a.vslot[e]);
+                        for (int e = e0[u]; e < e1; ++e) {
+                            const int slot = a.vslot[e];
+                            ST(slot, s - LD(slot));
+                            if (ET) hs[slot] = (uint8_t)(s < 0.0f);
+                        }
+                    }
+                    errs += (s < 0.0f);
+                    if (out_now) {
+                        if (a.post) a.post[(size_t)b * n + v] = s * Domain<ALGO>::out;
+                        if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
+                    }
                 }
             }
             if (MC) {
@@ -1015,6 +1073,228 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
             for (int i = tid; i <= iters; i += T) tr[i] = i <= it ? curve[i] : last;
         }
         if ((MC || a.its) && tid == 0) a.its[b] = it;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 2b'. Irregular graphs (variable degree <= 4, check degree <= 8), one codeword
+// per 1024-thread workgroup, host-built layout (build_irr_layout, capi.cpp):
+//   check c = k*1024 + t is thread t's row-k check; its slot j sits at position
+//   (k*DC + j)*1024 + t, so a row's reads and writes are lane-contiguous (LDS
+//   conflict-free, coalesced in the slab).  Absent slots (degree < DC) hold the
+//   rule's neutral input (sum-product wire a = 1, min-sum +inf) and are never
+//   written, so the update runs on DC entries without a degree test (x1 and
+//   min(+inf, .) change nothing: same values as oracle check_update_*(x, d)).
+//   Positions [0, S) are in LDS, [S, P) in a per-workgroup global slab (whole
+//   rows, so the row loop branches uniformly); the grid is one workgroup per CU
+//   so the slabs stay L2-resident.
+//   Lane p = i*1024 + t is thread t's i-th variable; lanes are sorted by degree
+//   and each degree class is padded to whole 64-lane rows, so "edge j present"
+//   is wave-uniform (readfirstlane).  Positions (2 x 16 bit per VGPR) and channel
+//   LLRs stay in VGPRs for the whole decode; one variable's messages may sit in
+//   LDS or in the slab (per-lane branch).
+//   ET: the variable phase XORs the hard decision of every negative posterior
+//   into a per-check syndrome bit array in LDS, tested after the phase.
+// ---------------------------------------------------------------------------
+template <int DC, int VPT, int ALGO, bool ET, bool MC>
+__global__ __launch_bounds__(kIrrT) void bp_irr_kernel(BpArgs a) {
+    constexpr int T = kIrrT;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int n = a.n, m = a.m, iters = a.max_iters, KC = a.irr_KC, S = a.irr_S;
+    lds_f32 *ml = (lds_f32 *)(lds_u8 *)smem;  // [S]
+    uint32_t *syn = reinterpret_cast<uint32_t *>(smem + (((size_t)S * 4 + 15) & ~(size_t)15));  // [m/32]
+    const int nsyn = (m + 31) >> 5;
+    int *curve = reinterpret_cast<int *>(syn + ((nsyn + 3) & ~3));  // [iters+1]
+    float *slab = a.scratch + (size_t)blockIdx.x * a.irr_P;
+    auto LD = [&](uint32_t q) -> float { return (int)q < S ? (float)ml[q] : slab[q]; };
+    auto ST = [&](uint32_t q, float x) {
+        if ((int)q < S) ml[q] = x;
+        else slab[q] = x;
+    };
+    constexpr float neutral = ALGO == 0 ? 1.0f : __builtin_inff();
+    const uint64_t cd = (uint32_t)a.irr_cdeg[tid] | ((uint64_t)(uint32_t)a.irr_cdeg[T + tid] << 32);
+    uint32_t pp[2 * VPT];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        pp[2 * i] = (uint32_t)a.irr_lane[(size_t)T * VPT + i * T + tid];
+        pp[2 * i + 1] = (uint32_t)a.irr_lane[(size_t)2 * T * VPT + i * T + tid];
+    }
+    auto POS = [&](int i, int j) -> uint32_t {
+        const uint32_t w = pp[2 * i + (j >> 1)];
+        return (j & 1) ? (w >> 16) : (w & 0xFFFFu);
+    };
+
+    for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+        const uint64_t cw = a.first_cw + (uint64_t)b;
+        __syncthreads();  // previous codeword drained (messages, curve, syndrome)
+        if (MC) {
+            for (int i = tid; i <= iters; i += T) curve[i] = 0;
+        }
+        // absent check slots -> neutral
+        for (int k = 0; k < KC; ++k) {
+            const int d = (int)((cd >> (4 * k)) & 15u);
+            for (int j = d; j < DC; ++j) ST((uint32_t)((k * DC + j) * T + tid), neutral);
+        }
+        // channel LLRs and the first variable-to-check messages
+        float L[VPT];
+        int err0 = 0;
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            const int v = a.irr_lane[i * T + tid];
+            float l = 0.0f;
+            if (v >= 0) l = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
+            err0 += (v >= 0) & (l < 0.0f);
+            L[i] = l * Domain<ALGO>::in;
+            const float w = v2c_wire<ALGO>(L[i]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (__builtin_amdgcn_readfirstlane(POS(i, j)) != 0xFFFFu) ST(POS(i, j), w);
+        }
+        if (ET)
+            for (int i = tid; i < nsyn; i += T) syn[i] = 0u;
+        __syncthreads();
+        if (MC) {
+            const int w = wave_sum(err0);
+            if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[0], w);
+        }
+        float pr[(ET && !MC) ? VPT : 1];
+        if constexpr (ET && !MC) {
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) pr[i] = L[i];
+        }
+        // variable phase; FINAL = the last fixed-count iteration: outputs instead of messages
+        auto var_phase = [&](auto final_tag) {
+            constexpr bool FINAL = decltype(final_tag)::value;
+            int errs = 0;
+            // launder the packed positions: unpacked (and slab addresses) hoisted out
+            // of the iteration loop would need ~4*VPT more VGPRs
+#pragma unroll
+            for (int q = 0; q < 2 * VPT; ++q) asm volatile("" : "+v"(pp[q]));
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) {
+                bool has[4];
+                float cv[4];
+                float s = L[i];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    has[j] = __builtin_amdgcn_readfirstlane(POS(i, j)) != 0xFFFFu;
+                    cv[j] = has[j] ? LD(POS(i, j)) : 0.0f;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (has[j]) s += cv[j];
+                if constexpr (!FINAL) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (has[j]) ST(POS(i, j), v2c_wire<ALGO>(s - cv[j]));
+                }
+                if constexpr (ET) {
+                    if (s < 0.0f) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int q = (int)POS(i, j);
+                            if (has[j] && q < KC * DC * T) {  // a check slot (not a dummy)
+                                const int c = (q / (DC * T)) * T + (q % T);
+                                atomicXor(&syn[c >> 5], 1u << (c & 31));
+                            }
+                        }
+                    }
+                    if constexpr (!MC) pr[i] = s;
+                }
+                if constexpr (MC) errs += (s < 0.0f);
+                if constexpr (FINAL && !MC) {
+                    const int v = a.irr_lane[i * T + tid];
+                    if (v >= 0) {
+                        if (a.post) a.post[(size_t)b * n + v] = s * Domain<ALGO>::out;
+                        if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
+                    }
+                }
+            }
+            return errs;
+        };
+
+        int it = 0;
+        for (; it < iters; ++it) {
+            if (!ET && it > 0) __syncthreads();  // variable phase complete (ET: its syndrome barriers)
+            // ---- check phase ----
+            for (int k = 0; k < KC; ++k) {
+                const int d = (int)((cd >> (4 * k)) & 15u);
+                const int q0 = k * DC * T + tid;
+                float x[DC];
+                const bool in_lds = (k + 1) * DC * T <= S;  // uniform: whole rows
+                if (in_lds) {
+#pragma unroll
+                    for (int j = 0; j < DC; ++j) x[j] = ml[q0 + j * T];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < DC; ++j) x[j] = slab[q0 + j * T];
+                }
+                if constexpr (ALGO == 1 && DC == 6) check_update_ms6(x, a.alpha);
+                else check_update<ALGO, DC, true>(x, a.alpha);
+                if (in_lds) {
+#pragma unroll
+                    for (int j = 0; j < DC; ++j)
+                        if (j < d) ml[q0 + j * T] = x[j];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < DC; ++j)
+                        if (j < d) slab[q0 + j * T] = x[j];
+                }
+            }
+            __syncthreads();
+            // fixed-count decode: the last variable phase runs after the loop
+            if (!ET && !MC && it == iters - 1) break;
+            const int errs = var_phase(std::false_type{});
+            if (MC) {
+                const int w = wave_sum(errs);
+                if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[it + 1], w);
+            }
+            if constexpr (ET) {
+                __syncthreads();  // syndrome complete
+                int unsat = 0;
+                for (int i = tid; i < nsyn; i += T) unsat |= (syn[i] != 0u);
+                const bool more = __syncthreads_or(unsat);
+                for (int i = tid; i < nsyn; i += T) syn[i] = 0u;  // every read is before that barrier
+                if (!more) {
+                    ++it;
+                    break;
+                }
+            }
+        }
+        if (!ET && !MC && iters > 0) {
+            (void)var_phase(std::true_type{});
+            it = iters;
+        }
+        if constexpr (ET && !MC) {
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) {
+                const int v = a.irr_lane[i * T + tid];
+                if (v >= 0) {
+                    if (a.post) a.post[(size_t)b * n + v] = pr[i] * Domain<ALGO>::out;
+                    if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(pr[i] < 0.0f);
+                }
+            }
+        }
+        if (!ET && !MC && iters == 0) {
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) {
+                const int v = a.irr_lane[i * T + tid];
+                if (v >= 0) {
+                    if (a.post) a.post[(size_t)b * n + v] = L[i] * Domain<ALGO>::out;
+                    if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(L[i] < 0.0f);
+                }
+            }
+        }
+        if constexpr (MC) {
+            __syncthreads();
+            int32_t *tr = a.trial + (size_t)b * (iters + 1);
+            const int last = curve[it];
+            for (int i = tid; i <= iters; i += T) tr[i] = i <= it ? curve[i] : last;
+            if (tid == 0) a.its[b] = it;
+        } else {
+            if (a.its && tid == 0) a.its[b] = it;
+        }
     }
 }
 
@@ -1858,7 +2138,14 @@ BecArgs bec_args(const ldpc_graph &g) {
 }
 
 // --- soft path selection ---------------------------------------------------
-enum class BpPath { Lds36, Generic8, Generic16, Generic32, GenericG8, GenericG16, GenericG32, None };
+enum class BpPath { Lds36, Irr, Generic8, Generic16, Generic32, GenericG8, GenericG16, GenericG32, None };
+
+// bp_irr_kernel: LDS bytes (messages, syndrome bits, curve) and whether the slab is used
+size_t irr_lds_bytes(const ldpc_graph &g, int iters) {
+    const int nsyn = (g.m + 31) >> 5;
+    return (((size_t)g.irr_S * 4 + 15) & ~(size_t)15) + (size_t)((nsyn + 3) & ~3) * 4 + (size_t)(iters + 1) * 4;
+}
+bool irr_slab(const ldpc_graph &g) { return g.irr_S < g.irr_P; }
 
 size_t lds36_bytes(const ldpc_graph &g, int iters, bool et, bool mc) {
     const size_t Ep = (size_t)lds_pair_span(g.m, 6) + kLdsDummy;
@@ -1876,6 +2163,7 @@ BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc) {
     if (!g.consistent) return BpPath::None;
     if (g.lane_var && g.dv == 3 && g.dc == 6 && lds36_bytes(g, iters, et, mc) <= kLdsMax - 2048)
         return BpPath::Lds36;
+    if (g.irr_lane && irr_lds_bytes(g, iters) <= kLdsMax - 1024) return BpPath::Irr;
     const int d = g.max_cdeg;
     if (d > 32) return BpPath::None;
     const bool lds = generic_lds_bytes(g, iters, mc) <= kLdsMax - 2048;
@@ -1936,10 +2224,37 @@ hipError_t launch_generic(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int DC, int VPT, int ALGO, bool ET, bool MC>
+hipError_t launch_irr_shape(const ldpc_graph &g, const BpArgs &a, hipStream_t s) {
+    auto k = bp_irr_kernel<DC, VPT, ALGO, ET, MC>;
+    const size_t lds = irr_lds_bytes(g, a.max_iters);
+    hipError_t e = allow_lds(k, lds);
+    if (e != hipSuccess) return e;
+    const int grid = irr_slab(g) ? std::min(a.B, LDPC_GMEM_GRID) : a.B;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kIrrT), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int ALGO, bool ET, bool MC>
+hipError_t launch_irr(const ldpc_graph &g, BpArgs a, hipStream_t s) {
+    a.irr_lane = g.irr_lane;
+    a.irr_cdeg = g.irr_cdeg;
+    a.irr_KC = g.irr_KC;
+    a.irr_S = g.irr_S;
+    a.irr_P = g.irr_P;
+    if (irr_slab(g) && !a.scratch) return hipErrorInvalidValue;
+#define IRR_CASE(DC, VPT) \
+    if (g.irr_DC == DC && g.irr_VPT == VPT) return launch_irr_shape<DC, VPT, ALGO, ET, MC>(g, a, s);
+    IRR_CASE(6, 5) IRR_CASE(6, 10) IRR_CASE(6, 20) IRR_CASE(8, 5) IRR_CASE(8, 10) IRR_CASE(8, 20)
+#undef IRR_CASE
+    return hipErrorInvalidValue;
+}
+
 template <int ALGO, bool ET, bool MC>
 hipError_t dispatch_bp(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     switch (choose_path(g, a.max_iters, ET, MC)) {
         case BpPath::Lds36: return launch_lds36<ALGO, ET, MC>(g, a, s);
+        case BpPath::Irr: return launch_irr<ALGO, ET, MC>(g, a, s);
         case BpPath::Generic8: return launch_generic<8, ALGO, ET, MC, false>(g, a, s);
         case BpPath::Generic16: return launch_generic<16, ALGO, ET, MC, false>(g, a, s);
         case BpPath::Generic32: return launch_generic<32, ALGO, ET, MC, false>(g, a, s);
@@ -1987,15 +2302,19 @@ hipError_t launch_bec_decode(const ldpc_graph &g, uint8_t *d_words, int B, int m
 }
 
 size_t bp_scratch_bytes(const ldpc_graph &g, int B) {
-    const size_t per = ((size_t)g.E * 5 + (size_t)g.n * 4 + 15) & ~(size_t)15;
-    if (generic_lds_bytes(g, 0, true) + 4096 <= kLdsMax) return 0;
     const int grid = B < LDPC_GMEM_GRID ? B : LDPC_GMEM_GRID;
-    return per * (size_t)grid;
+    // the irregular kernel's slab (if any) and, for iteration counts that push
+    // it off LDS, the generic kernel's: enough for whichever path runs
+    const size_t irr = g.irr_lane && irr_slab(g) ? (size_t)g.irr_P * 4 * (size_t)grid : 0;
+    const size_t per = ((size_t)g.E * 5 + (size_t)g.n * 4 + 15) & ~(size_t)15;
+    const size_t gen = generic_lds_bytes(g, 0, true) + 4096 <= kLdsMax ? 0 : per * (size_t)grid;
+    return std::max(irr, gen);
 }
 
 const char *bp_kernel_name(const ldpc_graph &g, int early_stop) {
     switch (choose_path(g, 50, early_stop != 0, false)) {
         case BpPath::Lds36: return "bp_lds_kernel<3,6>";
+        case BpPath::Irr: return irr_slab(g) ? "bp_irr_kernel<lds+slab>" : "bp_irr_kernel<lds>";
         case BpPath::Generic8: return "bp_generic_kernel<8,lds>";
         case BpPath::Generic16: return "bp_generic_kernel<16,lds>";
         case BpPath::Generic32: return "bp_generic_kernel<32,lds>";
