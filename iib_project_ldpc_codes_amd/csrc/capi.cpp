@@ -313,10 +313,22 @@ bool build_irr_layout(const HostGraph &h, int &VPT, int &KC, int &DC, int &S, in
         const int c = slot_check[slot], j = slot - h.cptr[c];
         return ((c / T) * DC + j) * T + (c % T);
     };
+    // rows that fit LDS (whole rows; the rest go to the slab)
+    const int rows_lds = (int)std::min<size_t>((size_t)KC, kIrrLdsMsgBytes / ((size_t)DC * T * 4));
     std::vector<int> order(n);
     for (int v = 0; v < n; ++v) order[v] = v;
     auto deg = [&](int v) { return h.vptr[v + 1] - h.vptr[v]; };
-    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return deg(x) > deg(y); });
+    // within a degree class, lanes sorted by which of their edges live in the slab:
+    // a 64-lane row then mostly takes one side per edge (the other side's path is skipped)
+    auto slab_mask = [&](int v) {
+        int msk = 0;
+        for (int j = 0; j < deg(v); ++j)
+            if (slot_check[h.vslot[h.vptr[v] + j]] / T >= rows_lds) msk |= 1 << j;
+        return msk;
+    };
+    std::vector<int> key(n);
+    for (int v = 0; v < n; ++v) key[v] = -deg(v) * 64 + slab_mask(v);
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
     // lanes: degree classes padded to 64
     std::vector<int> lv;  // var id per lane, -(d+1) for a padding lane of degree d
     for (size_t a = 0; a < order.size();) {
@@ -350,7 +362,6 @@ bool build_irr_layout(const HostGraph &h, int &VPT, int &KC, int &DC, int &S, in
     P = dummy;
     if (P >= 0xFFFF) return false;
     // whole rows in LDS while they fit (the dummies too when everything fits)
-    const int rows_lds = (int)std::min<size_t>((size_t)KC, kIrrLdsMsgBytes / ((size_t)DC * T * 4));
     S = rows_lds == KC && (size_t)P * 4 <= kIrrLdsMsgBytes ? P : rows_lds * DC * T;
     cdeg.assign((size_t)2 * T, 0);
     for (int t = 0; t < T; ++t)

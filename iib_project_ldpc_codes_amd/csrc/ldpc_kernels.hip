@@ -903,6 +903,9 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 //   the outputs after every variable phase.
 // ---------------------------------------------------------------------------
 constexpr int kGenDV = 4;  // variable degrees up to this keep their messages in registers
+#ifndef LDPC_IRR_UV
+#define LDPC_IRR_UV 1  // variables per load batch in bp_irr_kernel's variable phase (2, 4: no faster)
+#endif
 #ifndef LDPC_GEN_UC
 #define LDPC_GEN_UC 2  // checks per step of the generic kernel's check phase (loads batched)
 #endif
@@ -1171,43 +1174,53 @@ __global__ __launch_bounds__(kIrrT) void bp_irr_kernel(BpArgs a) {
             // of the iteration loop would need ~4*VPT more VGPRs
 #pragma unroll
             for (int q = 0; q < 2 * VPT; ++q) asm volatile("" : "+v"(pp[q]));
+            // LDPC_IRR_UV variables per step: all their loads issue before the first
+            // store (stores and later loads may alias as far as the compiler knows)
 #pragma unroll
-            for (int i = 0; i < VPT; ++i) {
-                bool has[4];
-                float cv[4];
-                float s = L[i];
+            for (int i0 = 0; i0 < VPT; i0 += LDPC_IRR_UV) {
+                bool has[LDPC_IRR_UV][4];
+                float cv[LDPC_IRR_UV][4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    has[j] = __builtin_amdgcn_readfirstlane(POS(i, j)) != 0xFFFFu;
-                    cv[j] = has[j] ? LD(POS(i, j)) : 0.0f;
-                }
+                for (int u = 0; u < LDPC_IRR_UV; ++u)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (has[j]) s += cv[j];
-                if constexpr (!FINAL) {
+                    for (int j = 0; j < 4; ++j) {
+                        const int i = i0 + u;
+                        has[u][j] = i < VPT && __builtin_amdgcn_readfirstlane(POS(i < VPT ? i : 0, j)) != 0xFFFFu;
+                        cv[u][j] = has[u][j] ? LD(POS(i < VPT ? i : 0, j)) : 0.0f;
+                    }
+#pragma unroll
+                for (int u = 0; u < LDPC_IRR_UV; ++u) {
+                    const int i = i0 + u;
+                    if (i >= VPT) break;
+                    float s = L[i];
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        if (has[j]) ST(POS(i, j), v2c_wire<ALGO>(s - cv[j]));
-                }
-                if constexpr (ET) {
-                    if (s < 0.0f) {
+                        if (has[u][j]) s += cv[u][j];
+                    if constexpr (!FINAL) {
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int q = (int)POS(i, j);
-                            if (has[j] && q < KC * DC * T) {  // a check slot (not a dummy)
-                                const int c = (q / (DC * T)) * T + (q % T);
-                                atomicXor(&syn[c >> 5], 1u << (c & 31));
+                        for (int j = 0; j < 4; ++j)
+                            if (has[u][j]) ST(POS(i, j), v2c_wire<ALGO>(s - cv[u][j]));
+                    }
+                    if constexpr (ET) {
+                        if (s < 0.0f) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const int q = (int)POS(i, j);
+                                if (has[u][j] && q < KC * DC * T) {  // a check slot (not a dummy)
+                                    const int c = (q / (DC * T)) * T + (q % T);
+                                    atomicXor(&syn[c >> 5], 1u << (c & 31));
+                                }
                             }
                         }
+                        if constexpr (!MC) pr[i] = s;
                     }
-                    if constexpr (!MC) pr[i] = s;
-                }
-                if constexpr (MC) errs += (s < 0.0f);
-                if constexpr (FINAL && !MC) {
-                    const int v = a.irr_lane[i * T + tid];
-                    if (v >= 0) {
-                        if (a.post) a.post[(size_t)b * n + v] = s * Domain<ALGO>::out;
-                        if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
+                    if constexpr (MC) errs += (s < 0.0f);
+                    if constexpr (FINAL && !MC) {
+                        const int v = a.irr_lane[i * T + tid];
+                        if (v >= 0) {
+                            if (a.post) a.post[(size_t)b * n + v] = s * Domain<ALGO>::out;
+                            if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
+                        }
                     }
                 }
             }

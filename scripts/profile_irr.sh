@@ -11,7 +11,7 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 200 rocprofv3 --pmc $grp --kernel-include-regex bp_generic -f csv -d $OUT/pmc$i -o run -- python3 $CMD > $OUT/pmc$i.log 2>&1
+  timeout -k 10 200 rocprofv3 --pmc $grp --kernel-include-regex bp_irr -f csv -d $OUT/pmc$i -o run -- python3 $CMD > $OUT/pmc$i.log 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"; [ $rc -ge 124 ] && exit $rc
 done <<GROUPS
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU
