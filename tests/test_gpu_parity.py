@@ -363,25 +363,35 @@ def test_mc_bec_bitsliced_irregular_vs_scalar_kernel(torch):
     np.testing.assert_array_equal(got, c)
 
 
-def test_mc_minsum_bsc_exact(torch):
+@pytest.mark.parametrize("kind,early_stop", [("regular", True), ("csr", True), ("csr", False),
+                                             ("rsu20000", True), ("rsu20000", False)])
+def test_mc_minsum_bsc_exact(torch, kind, early_stop):
+    """Fused Monte-Carlo min-sum (channel + decode + per-iteration counts) against counters built
+    from the oracle: the (3,6) LDS kernel, the irregular kernel with every message in LDS (the
+    same code as CSR), and the irregular kernel with an L2 slab (RSU n = 20000)."""
+    from iib_project_ldpc_codes_amd import ensembles
     from iib_project_ldpc_codes_amd.graph import TannerGraph
-    g = TannerGraph.random_regular(1000, 3, 6, seed=23)
-    B, iters = 512, 20
-    got = _mc_counters(g, "bsc", 0.06, 8, B, iters, algo="minsum", alpha=0.75, early_stop=True)
+    if kind == "rsu20000":
+        g = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=5)
+        csr, B = g.to_csr(), 96
+    else:
+        g0 = TannerGraph.random_regular(1000, 3, 6, seed=23)
+        csr = oracle.csr_from_lists(g0.variable_lookup, g0.check_lookup, g0.n, g0.m, 3, 6)
+        g, B = (g0 if kind == "regular" else TannerGraph.from_csr(*csr)), 512
+    iters = 20
+    got = _mc_counters(g, "bsc", 0.06, 8, B, iters, algo="minsum", alpha=0.75, early_stop=early_stop)
     llr = oracle.channel(oracle.CH_BSC, 0.06, 8, 0, g.n, B)
-    csr = oracle.csr_from_lists(g.variable_lookup, g.check_lookup, g.n, g.m, 3, 6)
-    # per-iteration curve from the oracle: run 0..iters iterations with early stop
+    # per-iteration curve from the oracle: run 0..iters iterations
     want = np.zeros(4 + iters + 1, np.int64)
     want[0] = B
     want[4] = int((llr < 0).sum())
-    final_its = oracle.bp_decode_batch(csr, llr, iters, 1, alpha=0.75, early_stop=True)[2]
     for t in range(1, iters + 1):
-        _, h, _ = oracle.bp_decode_batch(csr, llr, t, 1, alpha=0.75, early_stop=True)
+        _, h, _ = oracle.bp_decode_batch(csr, llr, t, 1, alpha=0.75, early_stop=early_stop)
         want[4 + t] = int(h.sum())
-    _, h, _ = oracle.bp_decode_batch(csr, llr, iters, 1, alpha=0.75, early_stop=True)
+    _, h, its = oracle.bp_decode_batch(csr, llr, iters, 1, alpha=0.75, early_stop=early_stop)
     want[1] = int(h.any(axis=1).sum())
     want[2] = int(h.sum())
-    want[3] = int(final_its.sum())
+    want[3] = int(its.sum())
     np.testing.assert_array_equal(got, want)
 
 
