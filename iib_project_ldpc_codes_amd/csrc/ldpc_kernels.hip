@@ -903,6 +903,9 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 //   the outputs after every variable phase.
 // ---------------------------------------------------------------------------
 constexpr int kGenDV = 4;  // variable degrees up to this keep their messages in registers
+#ifndef LDPC_LDS36_GRID
+#define LDPC_LDS36_GRID 256  // persistent grid of the LDS kernel under early stop (one per CU)
+#endif
 #ifndef LDPC_IRR_UV
 #define LDPC_IRR_UV 1  // variables per load batch in bp_irr_kernel's variable phase (2, 4: no faster)
 #endif
@@ -2190,7 +2193,11 @@ hipError_t launch_lds36_vpt(const ldpc_graph &g, BpArgs a, size_t lds, hipStream
     auto k = bp_lds_kernel<3, 6, T, VPT, ALGO, ET, MC>;
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3(a.B), dim3(T), lds, s, a);
+    // with early stop, one persistent workgroup per CU looping over codewords beats a
+    // workgroup per codeword (+6 %: frames end at different iterations); fixed-count
+    // decodes are indifferent (within 0.4 %)
+    const int grid = ET && a.B > LDPC_LDS36_GRID ? LDPC_LDS36_GRID : a.B;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, s, a);
     return hipGetLastError();
 }
 
