@@ -515,6 +515,24 @@ int ldpc_debug_lane_layout(const int32_t *variable_to_check_list, const int32_t 
     return LDPC_OK;
 }
 
+int ldpc_debug_irr_layout(const int32_t *check_ptr, const int32_t *check_var, const int32_t *var_ptr,
+                          const int32_t *var_slot, int n, int m, int32_t *shape, int32_t *lane, int32_t *cdeg) {
+    LDPC_REQUIRE(shape, "null shape");
+    HostGraph h;
+    int rc = host_graph_from_csr(check_ptr, check_var, var_ptr, var_slot, n, m, h);
+    if (rc) return rc;
+    std::vector<int32_t> ln, cd;
+    int VPT = 0, KC = 0, DC = 0, S = 0, P = 0;
+    if (!h.consistent || !build_irr_layout(h, VPT, KC, DC, S, P, ln, cd)) {
+        set_error("graph outside the irregular kernel's range");
+        return LDPC_EUNSUP;
+    }
+    shape[0] = VPT; shape[1] = KC; shape[2] = DC; shape[3] = S; shape[4] = P;
+    if (lane) std::copy(ln.begin(), ln.end(), lane);
+    if (cdeg) std::copy(cd.begin(), cd.end(), cdeg);
+    return LDPC_OK;
+}
+
 const char *ldpc_bp_kernel_name(const ldpc_graph *g, int early_stop) {
     return g ? bp_kernel_name(*g, early_stop) : "none";
 }

@@ -251,6 +251,17 @@ int ldpc_debug_lane_layout(const int32_t *variable_to_check_list, const int32_t 
                            int n, int k, int dv, int dc, int32_t *T, int32_t *VPT, int32_t *lane_var,
                            int32_t *lane_slot);
 
+/*
+ * The irregular kernel's layout for a consistent CSR graph (ldpc_graph_create_csr
+ * arguments): shape[5] = {VPT, KC (check rows of 1024), DC (slots per check),
+ * S (positions in LDS), P (positions in all)}; lane int32[3][1024*VPT] (variable
+ * id or -1, positions of edges 0|1<<16 and 2|3<<16, 0xFFFF = none); cdeg
+ * int32[2][1024] (check degrees, 4 bits per row).  Returns LDPC_EUNSUP when the
+ * graph is outside the kernel's range.  Pass NULL arrays to query the shape.
+ */
+int ldpc_debug_irr_layout(const int32_t *check_ptr, const int32_t *check_var, const int32_t *var_ptr,
+                          const int32_t *var_slot, int n, int m, int32_t *shape, int32_t *lane, int32_t *cdeg);
+
 /* Name of the soft kernel a graph dispatches to (tests / bench). */
 const char *ldpc_bp_kernel_name(const ldpc_graph *g, int early_stop);
 

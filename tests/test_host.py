@@ -203,3 +203,58 @@ def test_oracle_sampler_attempts_geometric():
     """Whole-graph redraw: attempts ~ Geometric(P(valid)), P(valid) ~ exp(-5) for (3,6)."""
     a = np.array([oracle.sample_regular(1000, 3, 6, 7, g)[2] for g in range(200)])
     assert np.all(a > 0) and 90 < a.mean() < 250
+
+
+@pytest.mark.parametrize("kind", ["rsu20000", "rsu2000", "csr36"])
+def test_irregular_layout_invariants(kind):
+    """bp_irr_kernel's host layout (build_irr_layout): every CSR edge gets the position of its
+    check slot, positions are unique, 64-lane rows share a degree, check degrees round-trip,
+    whole rows live in LDS."""
+    from iib_project_ldpc_codes_amd import _native, ensembles
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    if kind.startswith("rsu"):
+        g = ensembles.sample_irregular(ensembles.RSU_DL4, int(kind[3:]), seed=3)
+        cptr, cvar, vptr, vslot = (np.ascontiguousarray(a, np.int32) for a in g.csr)
+    else:
+        g0 = TannerGraph.random_regular(1200, 3, 6, seed=2)
+        cptr, cvar, vptr, vslot = (np.ascontiguousarray(a, np.int32) for a in g0.to_csr())
+    n, m = len(vptr) - 1, len(cptr) - 1
+    L = _native.lib()
+    shape = np.zeros(5, np.int32)
+    assert L.ldpc_debug_irr_layout(cptr.ctypes.data, cvar.ctypes.data, vptr.ctypes.data, vslot.ctypes.data,
+                                   n, m, shape.ctypes.data, None, None) == 0
+    VPT, KC, DC, S, P = (int(x) for x in shape)
+    T = 1024
+    lane = np.zeros(3 * T * VPT, np.int32)
+    cdeg = np.zeros(2 * T, np.int32)
+    assert L.ldpc_debug_irr_layout(cptr.ctypes.data, cvar.ctypes.data, vptr.ctypes.data, vslot.ctypes.data,
+                                   n, m, shape.ctypes.data, lane.ctypes.data, cdeg.ctypes.data) == 0
+    var = lane[:T * VPT]
+    pos = np.stack([lane[T * VPT:2 * T * VPT] & 0xFFFF, (lane[T * VPT:2 * T * VPT] >> 16) & 0xFFFF,
+                    lane[2 * T * VPT:] & 0xFFFF, (lane[2 * T * VPT:] >> 16) & 0xFFFF], axis=1)
+    assert KC == (m + T - 1) // T and DC in (6, 8) and S <= P < 0xFFFF
+    assert S == P or S % (DC * T) == 0  # whole rows in LDS (or everything)
+    real = var >= 0
+    assert np.array_equal(np.sort(var[real]), np.arange(n))
+    deg = np.diff(vptr)
+    present = pos != 0xFFFF
+    np.testing.assert_array_equal(present[real].sum(axis=1), deg[var[real]])
+    # 64-lane rows: "edge j present" uniform
+    rows = present.reshape(-1, 64, 4)
+    assert np.all(rows.all(axis=1) | ~rows.any(axis=1))
+    # each present edge at its check slot's position; all positions distinct
+    slot_check = np.repeat(np.arange(m), np.diff(cptr))
+    for q in np.nonzero(real)[0][::7]:
+        v = var[q]
+        for j in range(deg[v]):
+            s_ = vslot[vptr[v] + j]
+            c = slot_check[s_]
+            assert pos[q, j] == ((c // T) * DC + (s_ - cptr[c])) * T + c % T
+    used = pos[present]
+    assert len(np.unique(used)) == len(used) and used.max() < P
+    # check degrees round-trip (4 bits per row)
+    cd = cdeg[:T].astype(np.uint32).astype(np.uint64) | (cdeg[T:].astype(np.uint32).astype(np.uint64) << np.uint64(32))
+    for k in range(KC):
+        c = k * T + np.arange(T)
+        want = np.where(c < m, np.diff(cptr)[np.minimum(c, m - 1)], 0)
+        np.testing.assert_array_equal((cd >> np.uint64(4 * k)) & np.uint64(15), want)
