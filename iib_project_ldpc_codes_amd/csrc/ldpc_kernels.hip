@@ -1417,7 +1417,7 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
 // exactly uniform.  Level 1 splits all sockets into K1 super-buckets (draws
 // ctr {(s>>8)<<6 | s&63, tag|att<<2|2, g}; stable scatter of variable ids as
 // u16 into the variable_lookup row, used as scratch); super-bucket i is then
-// staged into LDS and permuted by the one-level scheme with 512 buckets (draws
+// staged into LDS and permuted by the one-level scheme with 1024 buckets (draws
 // ctr {.., tag|i<<22|att<<2|0, g}, Fisher-Yates streams {t<<20|blk,
 // tag|i<<22|att<<2|1, g}) and written to its slot range.  Checks are validated
 // as soon as all their slots are final, so a bad attempt usually stops after a
@@ -1430,7 +1430,7 @@ __global__ __launch_bounds__(1024) void sample_big_kernel(SampleShape sh, uint32
                                                          uint64_t first_graph, int32_t *check_lookup,
                                                          int32_t *variable_lookup, int32_t *attempts,
                                                          int max_attempts) {
-    constexpr int T = 1024, NW = T / kWave, K2 = kBigK2, LOGK2 = 9, K1 = 1 << LOGK1;
+    constexpr int T = 1024, NW = T / kWave, K2 = kBigK2, LOGK2 = kBigK2Log, K1 = 1 << LOGK1;
     extern __shared__ __align__(16) unsigned char smem[];
     int *cnt2 = reinterpret_cast<int *>(smem);  // [K2][NW]
     int *cnt1 = cnt2 + K2 * NW;                  // [K1][NW]
