@@ -90,6 +90,30 @@ def cpu_baseline(graph, llr_host, seconds):
                       f"x{threads} threads (reference has no soft decoder)"}
 
 
+def valu_roofline(cw_iters_per_s):
+    """The unit that bounds the LDS kernel: vector-instruction issue.  VALU
+    wave-instructions per codeword-iteration come from the committed PMC profile of this kernel
+    (SQ_INSTS_VALU per launch / codeword-iterations); the live rate times that count is compared
+    with 256 CUs x 4 SIMDs issuing one wave64 VALU instruction per 4 cycles at 2.4 GHz
+    (transcendentals take 8, so frac understates the busy time: busy_frac_pmc is the profile's
+    SQ_ACTIVE_INST_VALU share at its own clock)."""
+    p = os.path.join(ROOT, "profiles", "r01c_pmc_summary.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    c, ns = d["counters"], d["dispatch_ns"]
+    per_it = c["SQ_INSTS_VALU"] / (BATCH * ITERS)
+    peak = 256 * 4 * 2.4e9 / 4
+    clock = c["GRBM_GUI_ACTIVE"] / 8 / (ns["GRBM_GUI_ACTIVE"] * 1e-9)
+    busy = c["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * ns["SQ_ACTIVE_INST_VALU"] * 1e-9 * clock)
+    achieved = per_it * cw_iters_per_s
+    return {"bound": "valu", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "G wave-instr/s",
+            "frac": achieved / peak, "valu_instr_per_codeword_iteration": per_it, "busy_frac_pmc": busy,
+            "note": "informational: the LDS-resident kernel is VALU-bound; instruction count from "
+                    "profiles/r01c_pmc_summary.json"}
+
+
 def load_traffic():
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(p):
@@ -251,6 +275,7 @@ def main():
                                  + " per codeword (channel LLRs in, posteriors + decisions out), not "
                                  f"{b_it * ITERS / 1e6:.0f} MB; the kernel is VALU-bound (DESIGN.md 3.1)"},
             "lds_roofline": lds_roofline(g.n, g.m, DC, DV, kernel_cw_iters),
+            "valu_roofline": valu_roofline(kernel_cw_iters),
             "cpu_baseline": cpu,
             "extras": extras,
         }
