@@ -28,6 +28,9 @@ constexpr int kWave = 64;
 #ifndef LDPC_BEC_BITS
 #define LDPC_BEC_BITS 1  // fixed-code BEC Monte-Carlo on the bit-sliced kernel when its planes fit LDS
 #endif
+#ifndef LDPC_BEC_DEC_BITS
+#define LDPC_BEC_DEC_BITS 1  // batch BEC decode (B >= 64) on the bit-sliced kernel when its planes fit LDS
+#endif
 #ifndef LDPC_ABLATE_CHECK
 #define LDPC_ABLATE_CHECK 0
 #endif
@@ -435,6 +438,206 @@ __global__ __launch_bounds__(T) void bec_mc_bits_kernel(BecArgs a, int B) {
     }
     __syncthreads();
     for (int i = tid; i < nloc; i += T) a.its[b0 + i] = itsl[i];
+}
+
+// ---------------------------------------------------------------------------
+// 1c. BEC batch decode, bit-sliced: bec_kernel's non-MC contract (arbitrary
+// words, caller errors[] accumulated and steering the stall test of
+// message_passing.c:16-19) for H = 4*sizeof(P) codewords per plane word.
+// A variable's word holds "erased" bits (low H) and value bits (high H, the
+// byte's bit 0 when not erased, 0 when erased); a check's word holds "exactly
+// one slot erased" bits (low) and the parity of its known bits (high), i.e.
+// bec_kernel's cs = ne==1 ? parity : 2.  Variable phase, in
+// variable_to_check_list order: sel = One[c] & erased & active,
+// val = (val & ~sel) | (parity & sel) -- the last known check message wins
+// (message_passing.c:55-62) -- and the variable is resolved iff some sel was set.
+// Codeword control (counts, stall test, zero-count break) is per codeword in
+// registers of lane i < NB; codewords that have stopped are masked out of the
+// variable phase ("active"), so a stalled word is frozen exactly as the
+// reference's early return leaves it.  When no codeword changed in an
+// iteration every active codeword is at a fixed point and its remaining
+// iterations (count fixed, caller errors[] still added and tested) are
+// replayed by its lane without touching the graph.
+// Output rewrites only the bytes that were 2 on input (a known byte is never
+// changed by the reference, whatever its value).
+// LDS: X[n][W], C[m][W] plane words, cnt[NB], act[W], 2 change flags, done.
+// ---------------------------------------------------------------------------
+template <int T, int W, typename P>
+__global__ __launch_bounds__(T) void bec_dec_bits_kernel(BecArgs a, int B) {
+    constexpr int H = 4 * (int)sizeof(P);  // codewords per plane word
+    constexpr uint32_t LO = (1u << H) - 1u;
+    constexpr int NB = H * W;  // codewords per workgroup (<= 64: control lanes in wave 0)
+    static_assert(NB <= kWave, "control lanes must sit in wave 0");
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1);
+    const int n = a.n, m = a.m, iters = a.max_iters;
+    P *Xv = reinterpret_cast<P *>(smem);  // [n][W]
+    P *Xc = Xv + (size_t)n * W;           // [m][W]
+    int *cnt = reinterpret_cast<int *>(smem + ((((size_t)n + m) * W * sizeof(P) + 15) & ~(size_t)15));  // [NB]
+    uint32_t *act = reinterpret_cast<uint32_t *>(cnt + NB);  // [W]
+    uint32_t *flag = act + W;                                 // [2] changed, [2] all stopped
+    const int64_t b0 = (int64_t)blockIdx.x * NB;
+    const int nloc = (int)min((int64_t)NB, (int64_t)B - b0);
+
+    for (int i = tid; i < NB; i += T) cnt[i] = 0;
+    if (tid < 3) flag[tid] = 0u;
+    if (tid < W) act[tid] = (1u << min(max(nloc - tid * H, 0), H)) - 1u;  // codewords with rows
+    __syncthreads();
+    // ---- words -> planes: thread (w, v) gathers byte v of the word's H rows (lanes = consecutive v) ----
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        int lc[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) lc[j] = 0;
+        for (int v = tid; v < n; v += T) {
+            uint32_t x = 0u;
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const int i = w * H + j;
+                const uint32_t y = i < nloc ? a.words[(size_t)(b0 + i) * n + v] : 0u;
+                const bool er = y == 2u;
+                x |= (uint32_t)er << j | (er ? 0u : (y & 1u)) << (H + j);
+                lc[j] += er;
+            }
+            Xv[(size_t)v * W + w] = (P)x;
+        }
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            const int s = wave_sum(lc[j]);
+            if (lane == 0 && s) atomicAdd(&cnt[w * H + j], s);
+        }
+    }
+    // control state of codeword tid (tid < nloc)
+    int p1 = 0, p2 = 0, its = iters;
+    bool done = tid >= nloc;
+    int32_t *er = a.errors + (size_t)(b0 + min(tid, max(nloc - 1, 0))) * iters;
+    __syncthreads();
+
+    for (int it = 0; it < iters; ++it) {
+        // ---- check phase (reads the previous planes only) ----
+        for (int c = tid; c < m; c += T) {
+            const int s0 = a.dc > 0 ? c * a.dc : a.cptr[c];
+            const int s1 = a.dc > 0 ? s0 + a.dc : a.cptr[c + 1];
+            uint32_t one[W], two[W], par[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) one[w] = two[w] = par[w] = 0u;
+            for (int s = s0; s < s1; ++s) {
+                uint32_t x[W];
+                bits_load<P, W>(Xv + (size_t)a.cvar[s] * W, x);
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint32_t e = x[w] & LO;
+                    two[w] |= one[w] & e;
+                    one[w] |= e;
+                    par[w] ^= x[w] >> H;
+                }
+            }
+#pragma unroll
+            for (int w = 0; w < W; ++w) one[w] = (one[w] & ~two[w]) | (par[w] & LO) << H;
+            bits_store<P, W>(Xc + (size_t)c * W, one);
+        }
+        __syncthreads();
+        // ---- variable phase: active erased variables take the last known check message ----
+        uint32_t av[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) av[w] = act[w];
+        uint32_t changed = 0u;
+        for (int v = tid; v < n; v += T) {
+            uint32_t x[W], any = 0u;
+            bits_load<P, W>(Xv + (size_t)v * W, x);
+#pragma unroll
+            for (int w = 0; w < W; ++w) any |= x[w] & av[w];
+            if (!any) continue;
+            const int e0 = a.dv > 0 ? v * a.dv : a.vptr[v];
+            const int e1 = a.dv > 0 ? e0 + a.dv : a.vptr[v + 1];
+            uint32_t val[W], res[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) val[w] = res[w] = 0u;
+            for (int e = e0; e < e1; ++e) {
+                const int c = a.vchk[e];
+                if (c < 0) continue;
+                uint32_t y[W];
+                bits_load<P, W>(Xc + (size_t)c * W, y);
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint32_t sel = y[w] & x[w] & av[w];  // low bits only (av)
+                    val[w] = (val[w] & ~sel) | ((y[w] >> H) & sel);
+                    res[w] |= sel;
+                }
+            }
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                x[w] = (x[w] & ~res[w]) | val[w] << H;
+                changed |= res[w];
+            }
+            bits_store<P, W>(Xv + (size_t)v * W, x);
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                uint32_t q = res[w];
+                while (q) {
+                    const int b = __builtin_ctz(q);
+                    q &= q - 1u;
+                    atomicSub(&cnt[w * H + b], 1);
+                }
+            }
+        }
+        if (__ballot(changed != 0u) && lane == 0) atomicOr(&flag[it & 1], 1u);
+        __syncthreads();
+        // ---- control: message_passing.c:70-78 per codeword, then the stall test of the next iteration ----
+        if (tid < kWave) {
+            if (!done) {
+                const bool chg = flag[it & 1] != 0u;
+                const int c = cnt[tid];
+                int cur = er[it] + c;
+                er[it] = cur;
+                p2 = p1;
+                p1 = cur;
+                if (c == 0) {
+                    done = true;
+                    its = it;
+                } else {
+                    for (int t = it + 1; t < iters; ++t) {
+                        if (t >= 2 && p1 == p2) {  // message_passing.c:16-19
+                            for (int j = t; j < iters; ++j) er[j] = p1;
+                            done = true;
+                            break;
+                        }
+                        if (chg) break;
+                        cur = er[t] + c;  // fixed point: replay iteration t
+                        er[t] = cur;
+                        p2 = p1;
+                        p1 = cur;
+                    }
+                    if (!chg) done = true;  // its stays iters
+                }
+            }
+            const uint64_t alive = __ballot(!done);
+            if (tid == 0) {
+#pragma unroll
+                for (int w = 0; w < W; ++w) act[w] = (uint32_t)(alive >> (w * H)) & LO;
+                flag[(it + 1) & 1] = 0u;
+                flag[2] = alive == 0ull;
+            }
+        }
+        __syncthreads();
+        if (flag[2]) break;
+    }
+    if (tid < nloc) a.its[b0 + tid] = its;
+    // ---- planes -> words: rewrite the bytes that were erased on input ----
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        for (int v = tid; v < n; v += T) {
+            const uint32_t x = Xv[(size_t)v * W + w];
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                const int i = w * H + j;
+                if (i < nloc) {
+                    uint8_t *p = a.words + (size_t)(b0 + i) * n + v;
+                    if (*p == 2u) *p = ((x >> j) & 1u) ? 2u : (uint8_t)((x >> (H + j)) & 1u);
+                }
+            }
+        }
+    }
 }
 
 // ===========================================================================
@@ -2128,6 +2331,40 @@ bool bec_bits_shape(const ldpc_graph &g, int B, int &W, int &T, int &bytes) {
     return bec_bits_lds_bytes(g, 1, 1) <= kLdsMax - 4096;
 }
 
+// bec_dec_bits_kernel: H = 16 (u32) or 4 (u8) codewords per plane word
+size_t bec_dec_bits_lds_bytes(const ldpc_graph &g, int W, int bytes_per_word) {
+    const int NB = 4 * bytes_per_word * W;
+    return ((((size_t)g.n + g.m) * W * bytes_per_word + 15) & ~(size_t)15) + (size_t)4 * NB + 4 * W + 16;
+}
+bool bec_dec_bits_shape(const ldpc_graph &g, int B, int &W, int &T, int &bytes) {
+    T = g.n > 4096 ? 512 : 256;
+    bytes = 4;
+    if (B < 64) return false;  // a few words (the drop-in's B = 1): one workgroup per codeword
+    for (int w : {4, 2, 1}) {
+        if (bec_dec_bits_lds_bytes(g, w, 4) <= 72 * 1024 && ((int64_t)B + 16 * w - 1) / (16 * w) >= 1024) {
+            W = w;
+            return true;
+        }
+    }
+    W = 1;
+    if (bec_dec_bits_lds_bytes(g, 1, 4) <= kLdsMax - 4096) return true;
+    T = 1024;
+    bytes = 1;
+    return bec_dec_bits_lds_bytes(g, 1, 1) <= kLdsMax - 4096;
+}
+
+template <int T, int W, typename P>
+hipError_t launch_bec_dec_bits(const ldpc_graph &g, const BecArgs &a, int B, hipStream_t stream) {
+    const size_t lds = bec_dec_bits_lds_bytes(g, W, (int)sizeof(P));
+    auto k = bec_dec_bits_kernel<T, W, P>;
+    hipError_t e = allow_lds(k, lds);
+    if (e != hipSuccess) return e;
+    constexpr int NB = 4 * (int)sizeof(P) * W;
+    const unsigned grid = (unsigned)(((int64_t)B + NB - 1) / NB);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, stream, a, B);
+    return hipGetLastError();
+}
+
 template <int T, int W, typename P>
 hipError_t launch_bec_bits(const ldpc_graph &g, const BecArgs &a, int B, hipStream_t stream) {
     const size_t lds = bec_bits_lds_bytes(g, W, (int)sizeof(P));
@@ -2318,6 +2555,18 @@ hipError_t launch_bec_decode(const ldpc_graph &g, uint8_t *d_words, int B, int m
     a.errors = d_errors;
     a.its = d_its;
     a.max_iters = max_iters;
+    int W = 0, T = 0, bytes = 0;
+    if (LDPC_BEC_DEC_BITS && bec_dec_bits_shape(g, B, W, T, bytes)) {
+        if (bytes == 1) return launch_bec_dec_bits<1024, 1, uint8_t>(g, a, B, stream);
+        if (T == 256) {
+            if (W == 4) return launch_bec_dec_bits<256, 4, uint32_t>(g, a, B, stream);
+            if (W == 2) return launch_bec_dec_bits<256, 2, uint32_t>(g, a, B, stream);
+            return launch_bec_dec_bits<256, 1, uint32_t>(g, a, B, stream);
+        }
+        if (W == 4) return launch_bec_dec_bits<512, 4, uint32_t>(g, a, B, stream);
+        if (W == 2) return launch_bec_dec_bits<512, 2, uint32_t>(g, a, B, stream);
+        return launch_bec_dec_bits<512, 1, uint32_t>(g, a, B, stream);
+    }
     return run_bec<false>(g, a, B, stream);
 }
 

@@ -75,12 +75,14 @@ def message_passing(word, iterations, v2c, c2v, n, k, dv, dc, errors=None):
     return w, err, it
 
 
-def bec_decode_batch(words, iterations, v2c, c2v, n, k, dv, dc):
-    words = np.ascontiguousarray(words, dtype=np.int8).copy()
+def bec_decode_batch(words, iterations, v2c, c2v, n, k, dv, dc, errors=None):
+    """errors: the caller's int32 [B, iterations] accumulators (zeros if None)."""
+    words = np.ascontiguousarray(words).astype(np.int8)
     B = words.shape[0]
     v2c = np.ascontiguousarray(v2c, dtype=np.int32).ravel()
     c2v = np.ascontiguousarray(c2v, dtype=np.int32).ravel()
-    err = np.zeros((B, iterations), np.int32)
+    err = (np.zeros((B, iterations), np.int32) if errors is None
+           else np.ascontiguousarray(errors, dtype=np.int32).reshape(B, iterations).copy())
     its = np.zeros(B, np.int32)
     lib().oracle_bec_decode_batch(_p(v2c), _p(c2v), n, k, dv, dc, _p(words), B, iterations, _p(err), _p(its))
     return words, err, its

@@ -89,7 +89,7 @@ def main():
         print(json.dumps({"workload": name, "batch": B, "decode_codewords_per_s": B / ms * 1e3,
                           "decode_ms": ms, "mc_codewords_per_s": B / mc_ms * 1e3, "mean_iterations": mean_its,
                           "fer": fer, "edge_visits_per_s": B / ms * 1e3 * mean_its * 2 * 3 * n,
-                          "cpu_baseline": cpu, "kernel": "bec_kernel"}), flush=True)
+                          "cpu_baseline": cpu, "kernel": "bec_dec_bits_kernel"}), flush=True)
 
 
 def mc_fixed(reps=3):

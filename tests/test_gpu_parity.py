@@ -123,6 +123,65 @@ def test_bec_irregular_csr_vs_oracle(torch):
     np.testing.assert_array_equal(its, oits)
 
 
+# Batches of >= 64 words run on bec_dec_bits_kernel (16 words per u32 plane
+# word, or 4 per byte for graphs whose u32 planes do not fit LDS).
+def test_bec_bitsliced_batch_reference_golden(golden):
+    """Every reference golden case (with and without caller errors[]), tiled to
+    130 words per (graph, max_its) so the batch takes the bit-sliced kernel with
+    a partial last workgroup; outputs must equal message_passing.c's."""
+    from iib_project_ldpc_codes_amd import decoder
+    graphs, cases = golden
+    groups = {}
+    for c in cases:
+        groups.setdefault((c["gi"], c["max_its"]), []).append(c)
+    for (gi, max_its), cs in groups.items():
+        g = _graph(golden, gi)
+        rows = [cs[i % len(cs)] for i in range(130)]
+        words = np.stack([c["word"] for c in rows]).astype(np.uint8)
+        errin = np.stack([np.zeros(max_its, np.int32) if c["errin"] is None else c["errin"].astype(np.int32)
+                          for c in rows])
+        w, err, its = decoder.bec_decode(g, words, max_its, errors=errin)
+        for b, c in enumerate(rows):
+            np.testing.assert_array_equal(w[b].astype(np.int8), c["out"])
+            np.testing.assert_array_equal(err[b], c["errors"][1:] if c["errin"] is None else c["errors"])
+            assert its[b] == c["it"], (gi, max_its, b)
+
+
+def _perturbed_bec_batch(n, B, eps, iters, seed):
+    """Channel words with some rows corrupted (known bits flipped, so checks
+    disagree and the last known message decides) and some rows given small
+    caller errors[] that make the reference's stall test fire early."""
+    rng = np.random.default_rng(seed)
+    words = oracle.channel(oracle.CH_BEC, eps, seed, 0, n, B).astype(np.uint8)
+    bad = rng.random((B, n)) < 0.002
+    bad[::5] = False
+    words[bad & (words != 2)] ^= 1
+    errin = np.zeros((B, iters), np.int32)
+    errin[::3] = rng.integers(0, 3, (len(errin[::3]), iters))
+    return words, errin
+
+
+@pytest.mark.parametrize("n,B,eps,iters,csr", [
+    (1000, 65536, 0.42, 50, False),   # u32 planes, 4 words per variable (64 codewords per workgroup)
+    (1000, 32768, 0.40, 20, False),   # 2 words
+    (1000, 130, 0.45, 50, True),      # 1 word, CSR graph, partial last workgroup
+    (10000, 256, 0.42, 60, False),    # 512 threads
+    (64800, 72, 0.42, 200, False),    # u8 planes (4 codewords per byte)
+])
+def test_bec_bitsliced_batch_vs_oracle(torch, n, B, eps, iters, csr):
+    from iib_project_ldpc_codes_amd import decoder
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g0 = TannerGraph.random_regular(n, 3, 6, seed=11)
+    g = TannerGraph.from_csr(*g0.to_csr()) if csr else g0
+    words, errin = _perturbed_bec_batch(n, B, eps, iters, seed=n + B)
+    w, err, its = decoder.bec_decode(g, words, iters, errors=errin)
+    ow, oerr, oits = oracle.bec_decode_batch(words, iters, g0.variable_lookup, g0.check_lookup, n, n // 2, 3, 6,
+                                             errors=errin)
+    np.testing.assert_array_equal(w.astype(np.int8), ow)
+    np.testing.assert_array_equal(err, oerr)
+    np.testing.assert_array_equal(its, oits)
+
+
 # ----------------------------------------------------------------- channels
 @pytest.mark.parametrize("n", [1000, 1003])
 def test_channels_vs_oracle(torch, n):
