@@ -2188,47 +2188,68 @@ __global__ __launch_bounds__(1024) void ml_kernel(const int32_t *__restrict__ cp
         // already in LDS once the pivot position is known.  cand/swp are double-
         // buffered by column parity, best[] triple-buffered (the atomicMin of column
         // j+1 may run before a slow thread reads best[] of column j).
-        int free_col = -1, shift = 0, b3 = 0;
-        for (int j = 0; j < ncols; ++j) {
-            const int buf = j & 1;
-            if ((j >> 6) != shift) {
-                ml_shift<W>(R);
+        int free_col = -1, shift = 0, b3 = 0, j = 0;
+        // One 64-column block at a time with the L = live words of the window only
+        // (words past the augmented column are zero in every row), so the column
+        // step is branch-free and its cost shrinks as the elimination advances.
+        auto block = [&](auto live_tag) {
+            constexpr int L = decltype(live_tag)::value;
+            const int jend = min(ncols, 64 * (shift + 1));
+            for (; j < jend; ++j) {
+                const int buf = j & 1;
+                const bool bit = (R[0] >> (j & 63)) & 1ull;
+                const uint64_t bal = __ballot(bit && tid >= j && tid < nrows);
+                if (bal && lane == (int)__ffsll((long long)bal) - 1) {
+                    uint64_t *cw = cand + (buf * NW + wave) * W;
+#pragma unroll
+                    for (int w = 0; w < L; ++w) cw[w] = R[w];
+                    atomicMin(&best[b3], tid);
+                }
+                if (tid == j) {
+#pragma unroll
+                    for (int w = 0; w < L; ++w) swp[buf * W + w] = R[w];
+                }
+                __syncthreads();
+                const int q = best[b3];
+                const int b_old = b3 == 0 ? 2 : b3 - 1;  // buffer of column j-1 == column j+2
+                if (tid == 0) best[b_old] = INT_MAX;
+                b3 = b3 == 2 ? 0 : b3 + 1;
+                if (q == INT_MAX) {
+                    free_col = j;
+                    return;
+                }
+                const uint64_t *pb = cand + (buf * NW + (q >> 6)) * W;
+                const bool take = (tid == j) && (q != j);               // row j becomes the pivot row
+                const uint64_t msk = (bit && tid != q) ? ~0ull : 0ull;  // rows holding bit j XOR it in
+#pragma unroll
+                for (int w = 0; w < L; ++w) {
+                    const uint64_t pw = pb[w];
+                    R[w] = take ? pw : (R[w] ^ (pw & msk));
+                }
+                if (tid == q && q != j) {  // the old row j moves to position q
+#pragma unroll
+                    for (int w = 0; w < L; ++w) R[w] = swp[buf * W + w];
+                }
+            }
+            if (j < ncols) {  // next block: drop the front word
+#pragma unroll
+                for (int w = 0; w + 1 < L; ++w) R[w] = R[w + 1];
+                R[L - 1] = 0;
                 ++shift;
             }
-            // all W words move every time (no per-word predicates: words past the
-            // window are zero in every row), so the column step is branch-free
-            const bool bit = (R[0] >> (j & 63)) & 1ull;
-            const uint64_t bal = __ballot(bit && tid >= j && tid < nrows);
-            if (bal && lane == (int)__ffsll((long long)bal) - 1) {
-                uint64_t *cw = cand + (buf * NW + wave) * W;
-#pragma unroll
-                for (int w = 0; w < W; ++w) cw[w] = R[w];
-                atomicMin(&best[b3], tid);
-            }
-            if (tid == j) {
-#pragma unroll
-                for (int w = 0; w < W; ++w) swp[buf * W + w] = R[w];
-            }
-            __syncthreads();
-            const int q = best[b3];
-            const int b_old = b3 == 0 ? 2 : b3 - 1;  // buffer of column j-1 == column j+2
-            if (tid == 0) best[b_old] = INT_MAX;
-            b3 = b3 == 2 ? 0 : b3 + 1;
-            if (q == INT_MAX) {
-                free_col = j;
-                break;
-            }
-            const uint64_t *pb = cand + (buf * NW + (q >> 6)) * W;
-            const bool take = (tid == j) && (q != j);           // row j becomes the pivot row
-            const uint64_t msk = (bit && tid != q) ? ~0ull : 0ull;  // rows holding bit j XOR it in
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint64_t pw = pb[w];
-                R[w] = take ? pw : (R[w] ^ (pw & msk));
-            }
-            if (tid == q && q != j) {  // the old row j moves to position q
-#pragma unroll
-                for (int w = 0; w < W; ++w) R[w] = swp[buf * W + w];
+        };
+        while (j < ncols && free_col < 0) {
+            switch (min(W, (ncols >> 6) - shift + 1)) {  // live words: columns [64*shift, ncols]
+#define LDPC_ML_LIVE(LL) \
+    case LL:             \
+        if constexpr (LL <= W) block(std::integral_constant<int, LL>{}); \
+        break;
+                LDPC_ML_LIVE(1) LDPC_ML_LIVE(2) LDPC_ML_LIVE(3) LDPC_ML_LIVE(4)
+                LDPC_ML_LIVE(5) LDPC_ML_LIVE(6) LDPC_ML_LIVE(7) LDPC_ML_LIVE(8)
+                LDPC_ML_LIVE(9) LDPC_ML_LIVE(10) LDPC_ML_LIVE(11) LDPC_ML_LIVE(12)
+                LDPC_ML_LIVE(13) LDPC_ML_LIVE(14) LDPC_ML_LIVE(15) LDPC_ML_LIVE(16)
+#undef LDPC_ML_LIVE
+                default: block(std::integral_constant<int, W>{});
             }
         }
         if (free_col < 0) {
