@@ -28,6 +28,9 @@ constexpr int kWave = 64;
 #ifndef LDPC_BEC_BITS
 #define LDPC_BEC_BITS 1  // fixed-code BEC Monte-Carlo on the bit-sliced kernel when its planes fit LDS
 #endif
+#ifndef LDPC_LDS36_PREFETCH
+#define LDPC_LDS36_PREFETCH 1  // persistent LDS kernel (decode API) prefetching the next codeword's LLRs
+#endif
 #ifndef LDPC_BEC_DEC_BITS
 #define LDPC_BEC_DEC_BITS 1  // batch BEC decode (B >= 64) on the bit-sliced kernel when its planes fit LDS
 #endif
@@ -886,6 +889,31 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
     const int lpos0 = (int)((uint32_t)(size_t)(lds_u8 *)smem >> 2);
     uint8_t *hsb = hs - lpos0;  // hsb[address >> 2] = hs[position]
 
+    // packed positions: codeword-independent, built once per workgroup
+    uint32_t sp[(NS + 1) / 2];
+#pragma unroll
+    for (int q = 0; q < (NS + 1) / 2; ++q) sp[q] = 0;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+#pragma unroll
+        for (int j = 0; j < DV; ++j) {
+            const int q = i * DV + j;
+            sp[q >> 1] |= (uint32_t)(a.lane_slot[(tid + i * T) * DV + j] + lpos0) << (16 * (q & 1));
+        }
+    }
+    // PF: the next codeword's channel LLRs are loaded into registers (v = tid + k*T,
+    // n <= VPT*T) while the current one writes its outputs, so a persistent
+    // workgroup never waits for HBM between codewords
+    constexpr bool PF = LDPC_LDS36_PREFETCH && !MC && !ET;  // (early stop: 2.6 % slower, not used)
+    float nx[PF ? VPT : 1];
+    if constexpr (PF) {
+#pragma unroll
+        for (int k = 0; k < VPT; ++k) {
+            const int v = tid + k * T;
+            nx[k] = v < n && (int)blockIdx.x < a.B ? a.llr[(size_t)blockIdx.x * n + v] : 0.0f;
+        }
+    }
+
     for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
         const uint64_t cw = a.first_cw + (uint64_t)b;
         // ---- stage the channel LLRs (coalesced) ----
@@ -894,27 +922,26 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             for (int i = tid; i <= iters; i += T) curve[i] = 0;
         }
         int err0 = 0;
-        for (int v = tid; v < n; v += T) {
-            const float l = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
-            msg[v] = l * Domain<ALGO>::in;
-            err0 += (l < 0.0f);
-        }
-        __syncthreads();
-        uint32_t sp[(NS + 1) / 2];
-        float L[VPT];
+        if constexpr (PF) {
 #pragma unroll
-        for (int q = 0; q < (NS + 1) / 2; ++q) sp[q] = 0;
-#pragma unroll
-        for (int i = 0; i < VPT; ++i) {
-            const int p = tid + i * T;
-            const int vv = a.lane_var[p];
-            L[i] = vv >= 0 ? msg[vv] : 0.0f;
-#pragma unroll
-            for (int j = 0; j < DV; ++j) {
-                const int q = i * DV + j;
-                sp[q >> 1] |= (uint32_t)(a.lane_slot[p * DV + j] + lpos0) << (16 * (q & 1));
+            for (int k = 0; k < VPT; ++k) {
+                const int v = tid + k * T;
+                if (v < n) msg[v] = nx[k] * Domain<ALGO>::in;
+            }
+        } else {
+            for (int v = tid; v < n; v += T) {
+                const float l = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
+                msg[v] = l * Domain<ALGO>::in;
+                err0 += (l < 0.0f);
             }
         }
+        int lv[VPT];
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) lv[i] = a.lane_var[tid + i * T];
+        __syncthreads();
+        float L[VPT];
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) L[i] = lv[i] >= 0 ? msg[lv[i]] : 0.0f;
         // absolute LDS byte address of my variable i's edge j, and the word there
         auto addr = [&](int i, int j) -> uint32_t {
             const int q = i * DV + j;
@@ -1072,6 +1099,14 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
         if (!ET && !MC && iters > 0) {
             (void)var_phase(std::true_type{});
             it = iters;
+        }
+        if constexpr (PF) {
+            const int bn = b + (int)gridDim.x;
+#pragma unroll
+            for (int k = 0; k < VPT; ++k) {
+                const int v = tid + k * T;
+                if (v < n && bn < a.B) nx[k] = a.llr[(size_t)bn * n + v];
+            }
         }
         if constexpr (MC) {
             __syncthreads();
@@ -2454,7 +2489,8 @@ hipError_t launch_lds36_vpt(const ldpc_graph &g, BpArgs a, size_t lds, hipStream
     // with early stop, one persistent workgroup per CU looping over codewords beats a
     // workgroup per codeword (+6 %: frames end at different iterations); fixed-count
     // decodes are indifferent (within 0.4 %)
-    const int grid = ET && a.B > LDPC_LDS36_GRID ? LDPC_LDS36_GRID : a.B;
+    const bool persistent = ET || (LDPC_LDS36_PREFETCH && !MC);  // fixed-count decode: +1 % with the prefetch
+    const int grid = persistent && a.B > LDPC_LDS36_GRID ? LDPC_LDS36_GRID : a.B;
     hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, s, a);
     return hipGetLastError();
 }
