@@ -31,6 +31,9 @@ constexpr int kWave = 64;
 #ifndef LDPC_LDS36_PREFETCH
 #define LDPC_LDS36_PREFETCH 1  // persistent LDS kernel (decode API) prefetching the next codeword's LLRs
 #endif
+#ifndef LDPC_SPA_PROD
+#define LDPC_SPA_PROD 1  // bp_lds_kernel sum-product without early stop: product-domain variable phase
+#endif
 #ifndef LDPC_BEC_DEC_BITS
 #define LDPC_BEC_DEC_BITS 1  // batch BEC decode (B >= 64) on the bit-sliced kernel when its planes fit LDS
 #endif
@@ -683,6 +686,22 @@ __device__ __forceinline__ float2 v2c_wire2(float2 x) {
     return x;
 }
 
+// Product domain (bp_lds_kernel PROD): for an extrinsic ratio R = 2^x the wire
+// value sign(x) (1 - 2^-min(|x|, 23)) of v2c_wire is (Rc - 1) / max(Rc, 1) with Rc =
+// R clamped to [2^-23, 2^23]: one v_rcp_f32 in place of the v_exp_f32.
+__device__ __forceinline__ float ratio_wire(float R) {
+    const float lo = __builtin_amdgcn_fmed3f(R, 0x1p-23f, 0x1p23f);
+    const float hi = __builtin_amdgcn_fmed3f(R, 1.0f, 0x1p23f);
+    return (lo - 1.0f) * __builtin_amdgcn_rcpf(hi);
+}
+__device__ __forceinline__ float2 ratio_wire2(float2 R) {
+    const float2 lo = make_float2(__builtin_amdgcn_fmed3f(R.x, 0x1p-23f, 0x1p23f),
+                                  __builtin_amdgcn_fmed3f(R.y, 0x1p-23f, 0x1p23f));
+    const float2 hi = make_float2(__builtin_amdgcn_fmed3f(R.x, 1.0f, 0x1p23f),
+                                  __builtin_amdgcn_fmed3f(R.y, 1.0f, 0x1p23f));
+    return (lo - make_float2(1.0f, 1.0f)) * make_float2(__builtin_amdgcn_rcpf(hi.x), __builtin_amdgcn_rcpf(hi.y));
+}
+
 // Check-node update over D messages in registers; entries i >= d are padding
 // (+inf for min-sum, unit factors for sum-product).  Same product / min order as
 // oracle check_update_{spa,ms}: min-sum is bit-exact with it, sum-product agrees
@@ -776,7 +795,10 @@ __device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
     return make_float2(r.x, r.y);
 }
 
-template <int D>
+// LOG = false (product-domain variable phase, bp_lds_kernel's PROD): the output
+// is the ratio (D+N)/(D-N) itself, i.e. 2^message; the log moves to the variable
+// phase's final posterior.
+template <int D, bool LOG = true>
 __device__ __forceinline__ void check_update_spa_pair(float2 (&a)[D]) {
     float2 b[D];
 #pragma unroll
@@ -796,6 +818,7 @@ __device__ __forceinline__ void check_update_spa_pair(float2 (&a)[D]) {
         const float2 P = pk_fma(pdj, sdj, N);
         const float2 Q = pk_fma(pdj, sdj, make_float2(-N.x, -N.y));
         const float2 r = P * make_float2(__builtin_amdgcn_rcpf(Q.x), __builtin_amdgcn_rcpf(Q.y));
+        if constexpr (!LOG) return r;
         return make_float2(__builtin_amdgcn_logf(r.x), __builtin_amdgcn_logf(r.y));
     };
     const float2 one = make_float2(1.0f, 1.0f);
@@ -968,6 +991,121 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 #pragma unroll
             for (int i = 0; i < VPT; ++i) pr[i] = L[i];
         }
+        // PROD (sum-product, no early stop): L holds E = 2^channel from here on, the
+        // check phase leaves ratios r = 2^c2v in LDS, and the variable phase forms
+        // each edge's extrinsic ratio E * prod_{k != j} r_k by prefix / suffix
+        // products -- no v_log_f32 per edge in the check phase, a v_rcp_f32 in place
+        // of the v_exp_f32 here.  The posterior (FINAL) is L + sum log2 r_j in the
+        // log-domain order, L = log2(E); MC tests post < 1.
+        constexpr bool PROD = LDPC_SPA_PROD && ALGO == 0;
+        if constexpr (PROD) {
+#pragma unroll
+            for (int i = 0; i < VPT; ++i) L[i] = __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[i], -126.0f, 126.0f));
+        }
+        auto llr_log2 = [&](int i) -> float {  // PROD: channel LLR of lane i, message units
+            // log2(E) restores it to ~1e-7 absolute; a value clamped at staging
+            // (|LLR| > 87 nats) is re-read from the input instead
+            float l = __builtin_amdgcn_logf(L[i]);
+            if (__builtin_expect(fabsf(l) >= 126.0f, 0)) {
+                const int vv = a.lane_var[tid + i * T];
+                l = vv >= 0 && !MC ? a.llr[(size_t)b * n + vv] * Domain<ALGO>::in : 0.0f;
+            }
+            return l;
+        };
+        auto var_phase_prod = [&](auto final_tag) {
+            constexpr bool FINAL = decltype(final_tag)::value;
+            int errs = 0;
+            auto edges = [&](auto &cv, auto Ev, auto at_j, auto put_j) {
+                // cv[j]: ratios of this variable's edges; put_j(j, wire)
+                decltype(Ev) pre[DV];
+                pre[0] = Ev;
+#pragma unroll
+                for (int j = 1; j < DV; ++j) pre[j] = pre[j - 1] * cv[j - 1];
+                auto suf = cv[DV - 1];
+                put_j(DV - 1, pre[DV - 1]);
+#pragma unroll
+                for (int j = DV - 2; j >= 0; --j) {
+                    put_j(j, pre[j] * suf);
+                    if (j > 0) suf = suf * cv[j];
+                }
+                (void)at_j;
+                return pre[DV - 1] * cv[DV - 1];  // posterior ratio
+            };
+#pragma unroll
+            for (int i = 0; i + 1 < VPT; i += 2) {
+                uint32_t a0[DV], a1[DV];
+                float2 cv[DV];
+#pragma unroll
+                for (int j = 0; j < DV; ++j) {
+                    a0[j] = addr(i, j);
+                    a1[j] = addr(i + 1, j);
+                }
+#pragma unroll
+                for (int j = 0; j < DV; ++j) cv[j] = make_float2(at(a0[j]), at(a1[j]));
+                if constexpr (FINAL) {
+                    float2 s = make_float2(llr_log2(i), llr_log2(i + 1));
+#pragma unroll
+                    for (int j = 0; j < DV; ++j)
+                        s = s + make_float2(__builtin_amdgcn_logf(cv[j].x), __builtin_amdgcn_logf(cv[j].y));
+                    if constexpr (!MC) { pr[i] = s.x; pr[i + 1] = s.y; }
+                } else {
+                    const float2 post = edges(cv, make_float2(L[i], L[i + 1]), 0, [&](int j, float2 R) {
+                        const float2 w = ratio_wire2(R);
+                        at(a0[j]) = w.x;
+                        at(a1[j]) = w.y;
+                    });
+                    if constexpr (ET) {
+#pragma unroll
+                        for (int j = 0; j < DV; ++j) {
+                            hsb[a0[j] >> 2] = (uint8_t)(post.x < 1.0f);
+                            hsb[a1[j] >> 2] = (uint8_t)(post.y < 1.0f);
+                        }
+                        if constexpr (!MC) {  // prod r_j (no E: cannot overflow); logged at the end
+                            float2 pq = cv[0];
+#pragma unroll
+                            for (int j = 1; j < DV; ++j) pq = pq * cv[j];
+                            pr[i] = pq.x;
+                            pr[i + 1] = pq.y;
+                        }
+                    }
+                    if constexpr (MC)
+                        errs += ((a0[0] < 4u * (E + lpos0)) & (post.x < 1.0f)) + ((a1[0] < 4u * (E + lpos0)) & (post.y < 1.0f));
+                    else (void)post;
+                }
+                if (LDPC_VAR_PAIRS > 0 && (i / 2) % LDPC_VAR_PAIRS == LDPC_VAR_PAIRS - 1)
+                    __builtin_amdgcn_sched_barrier(0);
+            }
+            if constexpr (VPT % 2 == 1) {
+                constexpr int i = VPT - 1;
+                uint32_t a0[DV];
+                float cv[DV];
+#pragma unroll
+                for (int j = 0; j < DV; ++j) a0[j] = addr(i, j);
+#pragma unroll
+                for (int j = 0; j < DV; ++j) cv[j] = at(a0[j]);
+                if constexpr (FINAL) {
+                    float s = llr_log2(i);
+#pragma unroll
+                    for (int j = 0; j < DV; ++j) s += __builtin_amdgcn_logf(cv[j]);
+                    if constexpr (!MC) pr[i] = s;
+                } else {
+                    const float post = edges(cv, L[i], 0, [&](int j, float R) { at(a0[j]) = ratio_wire(R); });
+                    if constexpr (ET) {
+#pragma unroll
+                        for (int j = 0; j < DV; ++j) hsb[a0[j] >> 2] = (uint8_t)(post < 1.0f);
+                        if constexpr (!MC) {
+                            float pq = cv[0];
+#pragma unroll
+                            for (int j = 1; j < DV; ++j) pq *= cv[j];
+                            pr[i] = pq;
+                        }
+                    }
+                    if constexpr (MC) errs += (a0[0] < 4u * (E + lpos0)) & (post < 1.0f);
+                    else (void)post;
+                }
+            }
+            return errs;
+        };
         auto var_phase = [&](auto final_tag) {
             constexpr bool FINAL = decltype(final_tag)::value;
             int errs = 0;
@@ -1064,7 +1202,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                 for (int i = 0; i < DC; ++i) x2[i] = x2[i] * make_float2(0.5f, 0.5f);  // timing ablation only
 #else
                 if constexpr (ALGO == 0) {
-                    check_update_spa_pair<DC>(x2);
+                    check_update_spa_pair<DC, !PROD>(x2);
                 } else {
                     float xa[DC], xb[DC];
 #pragma unroll
@@ -1090,14 +1228,19 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             }
             // fixed-count decode: the last variable phase runs after the loop
             if (!ET && !MC && it == iters - 1) break;
-            const int errs = (LDPC_ABLATE_PHASE == 2) ? 0 : var_phase(std::false_type{});
+            int errs = 0;
+            if constexpr (LDPC_ABLATE_PHASE != 2) {
+                if constexpr (PROD) errs = var_phase_prod(std::false_type{});
+                else errs = var_phase(std::false_type{});
+            }
             if (MC) {
                 const int w = wave_sum(errs);
                 if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[it + 1], w);
             }
         }
         if (!ET && !MC && iters > 0) {
-            (void)var_phase(std::true_type{});
+            if constexpr (PROD) (void)var_phase_prod(std::true_type{});
+            else (void)var_phase(std::true_type{});
             it = iters;
         }
         if constexpr (PF) {
@@ -1106,6 +1249,12 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             for (int k = 0; k < VPT; ++k) {
                 const int v = tid + k * T;
                 if (v < n && bn < a.B) nx[k] = a.llr[(size_t)bn * n + v];
+            }
+        }
+        if constexpr (PROD && ET && !MC) {  // early stop: posterior = L + log2(prod r_j)
+            if (iters > 0) {
+#pragma unroll
+                for (int i = 0; i < VPT; ++i) pr[i] = llr_log2(i) + __builtin_amdgcn_logf(pr[i]);
             }
         }
         if constexpr (MC) {
