@@ -97,7 +97,7 @@ def valu_roofline(cw_iters_per_s):
     with 256 CUs x 4 SIMDs issuing one wave64 VALU instruction per 4 cycles at 2.4 GHz
     (transcendentals take 8, so frac understates the busy time: busy_frac_pmc is the profile's
     SQ_ACTIVE_INST_VALU share at its own clock)."""
-    p = os.path.join(ROOT, "profiles", "r01e_pmc_summary.json")
+    p = os.path.join(ROOT, "profiles", "r01f_pmc_summary.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
@@ -111,7 +111,7 @@ def valu_roofline(cw_iters_per_s):
     return {"bound": "valu", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "G wave-instr/s",
             "frac": achieved / peak, "valu_instr_per_codeword_iteration": per_it, "busy_frac_pmc": busy,
             "note": "informational: the LDS-resident kernel is VALU-bound; instruction count from "
-                    "profiles/r01e_pmc_summary.json"}
+                    "profiles/r01f_pmc_summary.json"}
 
 
 def load_traffic():

@@ -34,6 +34,9 @@ constexpr int kWave = 64;
 #ifndef LDPC_SPA_PROD
 #define LDPC_SPA_PROD 1  // bp_lds_kernel sum-product without early stop: product-domain variable phase
 #endif
+#ifndef LDPC_WIRE_MUL
+#define LDPC_WIRE_MUL 0  // 1: PROD wire as (Rc - 1) / max(Rc, 1) (one more packed op per two edges)
+#endif
 #ifndef LDPC_BEC_DEC_BITS
 #define LDPC_BEC_DEC_BITS 1  // batch BEC decode (B >= 64) on the bit-sliced kernel when its planes fit LDS
 #endif
@@ -687,8 +690,11 @@ __device__ __forceinline__ float2 v2c_wire2(float2 x) {
 }
 
 // Product domain (bp_lds_kernel PROD): for an extrinsic ratio R = 2^x the wire
-// value sign(x) (1 - 2^-min(|x|, 23)) of v2c_wire is (Rc - 1) / max(Rc, 1) with Rc =
-// R clamped to [2^-23, 2^23]: one v_rcp_f32 in place of the v_exp_f32.
+// value sign(x) (1 - 2^-min(|x|, 23)) of v2c_wire is
+//   min(R, 1) - min(1/R, 1)   (R >= 1: 1 - 1/R;  R < 1: R - 1)
+// with both terms clamped below at 2^-23 (|x| <= 23): two v_med3_f32, one
+// v_rcp_f32 in place of the v_exp_f32, one packed subtraction per two edges.
+#if LDPC_WIRE_MUL
 __device__ __forceinline__ float ratio_wire(float R) {
     const float lo = __builtin_amdgcn_fmed3f(R, 0x1p-23f, 0x1p23f);
     const float hi = __builtin_amdgcn_fmed3f(R, 1.0f, 0x1p23f);
@@ -701,6 +707,19 @@ __device__ __forceinline__ float2 ratio_wire2(float2 R) {
                                   __builtin_amdgcn_fmed3f(R.y, 1.0f, 0x1p23f));
     return (lo - make_float2(1.0f, 1.0f)) * make_float2(__builtin_amdgcn_rcpf(hi.x), __builtin_amdgcn_rcpf(hi.y));
 }
+#else
+__device__ __forceinline__ float ratio_wire(float R) {
+    return __builtin_amdgcn_fmed3f(R, 0x1p-23f, 1.0f) -
+           __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(R), 0x1p-23f, 1.0f);
+}
+__device__ __forceinline__ float2 ratio_wire2(float2 R) {
+    const float2 lo = make_float2(__builtin_amdgcn_fmed3f(R.x, 0x1p-23f, 1.0f),
+                                  __builtin_amdgcn_fmed3f(R.y, 0x1p-23f, 1.0f));
+    const float2 u = make_float2(__builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(R.x), 0x1p-23f, 1.0f),
+                                 __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(R.y), 0x1p-23f, 1.0f));
+    return lo - u;
+}
+#endif
 
 // Check-node update over D messages in registers; entries i >= d are padding
 // (+inf for min-sum, unit factors for sum-product).  Same product / min order as
