@@ -37,6 +37,9 @@ constexpr int kWave = 64;
 #ifndef LDPC_WIRE_MUL
 #define LDPC_WIRE_MUL 0  // 1: PROD wire as (Rc - 1) / max(Rc, 1) (one more packed op per two edges)
 #endif
+#ifndef LDPC_MS_LAUNDER
+#define LDPC_MS_LAUNDER 1  // min-sum: scaled minima computed once per check (see check_update_ms6)
+#endif
 #ifndef LDPC_BEC_DEC_BITS
 #define LDPC_BEC_DEC_BITS 1  // batch BEC decode (B >= 64) on the bit-sliced kernel when its planes fit LDS
 #endif
@@ -796,7 +799,12 @@ __device__ __forceinline__ void check_update_ms6(float (&x)[6], float alpha) {
     const float mn1 = fminf(fminf(ax[0], ax[1]), ax[2]), md1 = __builtin_amdgcn_fmed3f(ax[0], ax[1], ax[2]);
     const float mn2 = fminf(fminf(ax[3], ax[4]), ax[5]), md2 = __builtin_amdgcn_fmed3f(ax[3], ax[4], ax[5]);
     const float m1 = fminf(mn1, mn2), m2 = fminf(fminf(fmaxf(mn1, mn2), md1), md2);
-    const float am1 = alpha * m1, am2 = alpha * m2;
+    float am1 = alpha * m1, am2 = alpha * m2;
+#if LDPC_MS_LAUNDER
+    // keep the two products: otherwise select(alpha*m2, alpha*m1) is folded into
+    // alpha*select(m2, m1), one multiply per edge instead of two per check
+    asm volatile("" : "+v"(am1), "+v"(am2));
+#endif
     bool neg = false;
 #pragma unroll
     for (int i = 0; i < 6; ++i) neg ^= (x[i] < 0.0f);
