@@ -429,6 +429,28 @@ def test_mc_bec_bitsliced_shapes_exact(torch, n, B, X, stop):
     np.testing.assert_array_equal(got, want)
 
 
+def _bec_decode_scalar(decoder, g, words, iters, errors=None, chunk=32):
+    """Batch decode in chunks of < 64 words: the per-codeword bec_kernel path."""
+    outs = [decoder.bec_decode(g, words[i:i + chunk], iters,
+                               errors=None if errors is None else errors[i:i + chunk])
+            for i in range(0, len(words), chunk)]
+    return tuple(np.concatenate([o[k] for o in outs]) for k in range(3))
+
+
+def test_bec_bitsliced_batch_irregular_vs_scalar_kernel(torch):
+    """Irregular CSR graph (RSU, variable degrees 2-4, check degrees up to 8): the
+    bit-sliced batch decoder == the per-codeword kernel (pinned to the oracle on CSR
+    graphs) on perturbed words with caller errors[]."""
+    from iib_project_ldpc_codes_amd import decoder, ensembles
+    g = ensembles.sample_irregular(ensembles.RSU_DL4, 2000, seed=5)
+    words, errin = _perturbed_bec_batch(g.n, 1000, 0.44, 40, seed=77)
+    w, err, its = decoder.bec_decode(g, words, 40, errors=errin)
+    sw, serr, sits = _bec_decode_scalar(decoder, g, words, 40, errors=errin)
+    np.testing.assert_array_equal(w, sw)
+    np.testing.assert_array_equal(err, serr)
+    np.testing.assert_array_equal(its, sits)
+
+
 def test_mc_bec_bitsliced_irregular_vs_scalar_kernel(torch):
     """Irregular CSR graph: bit-sliced MC counters == counters built from the per-codeword
     BEC kernel (itself pinned to the oracle by test_bec_irregular_csr_vs_oracle)."""
@@ -437,7 +459,7 @@ def test_mc_bec_bitsliced_irregular_vs_scalar_kernel(torch):
     B, iters, eps = 8192, 60, 0.45
     got = _mc_counters(g, "bec", eps, 31, B, iters)
     words = oracle.channel(oracle.CH_BEC, eps, 31, 0, g.n, B)
-    _, err, its = decoder.bec_decode(g, words.astype(np.uint8), iters)
+    _, err, its = _bec_decode_scalar(decoder, g, words.astype(np.uint8), iters)
     c = np.zeros(4 + iters + 1, np.int64)
     curves = np.concatenate([np.count_nonzero(words == 2, axis=1)[:, None], err], axis=1)
     c[0] = B
