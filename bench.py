@@ -237,6 +237,33 @@ def main():
             extras[key] = {"codewords_per_s": Bb / (a.elapsed_time(b) * 1e-3),
                            "mean_iterations": float(its_bec.float().mean().item()), "batch": Bb}
             del w, w0
+        # configs[3] shape: irregular RSU rate-1/2 ensemble (density-evolution lambda/rho),
+        # n = 20000, BI-AWGN sum-product, 100 iterations, fixed count and with early stop
+        from iib_project_ldpc_codes_amd import ensembles
+        gi = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1)
+        Bi = 8192
+        llr_i = decoder.channel_dev("awgn", 0.80, 7, 0, gi.n, Bi)
+        for key, et in (("irregular_cfg4_n20000_spa_100it", False), ("irregular_cfg4_n20000_spa_early_stop", True)):
+            _, _, its_i = decoder.bp_decode_dev(gi, llr_i, 100, "spa", early_stop=et, want_post=False)
+            torch.cuda.synchronize()
+            a.record(stream)
+            _, _, its_i = decoder.bp_decode_dev(gi, llr_i, 100, "spa", early_stop=et, want_post=False)
+            b.record(stream)
+            torch.cuda.synchronize()
+            extras[key] = {"codewords_per_s": Bi / (a.elapsed_time(b) * 1e-3), "batch": Bi, "sigma": 0.80,
+                           "mean_iterations": float(its_i.float().mean().item()),
+                           "kernel": gi.kernel_name(early_stop=et)}
+        del llr_i
+        # "optimal" modes: ML erasure decoding (parallel_simulator.py:60-129), n = 1000, eps = 0.45
+        gm = TannerGraph.random_regular(1000, DV, DC, seed=1)
+        wm = decoder.channel_dev("bec", 0.45, 5, 0, gm.n, 32768)
+        decoder.ml_decode_dev(gm, wm)
+        torch.cuda.synchronize()
+        a.record(stream)
+        decoder.ml_decode_dev(gm, wm)
+        b.record(stream)
+        torch.cuda.synchronize()
+        extras["ml_n1000_eps0.45"] = {"words_per_s": 32768 / (a.elapsed_time(b) * 1e-3), "batch": 32768}
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1:
