@@ -34,9 +34,6 @@ constexpr int kWave = 64;
 #ifndef LDPC_SPA_PROD
 #define LDPC_SPA_PROD 1  // bp_lds_kernel sum-product without early stop: product-domain variable phase
 #endif
-#ifndef LDPC_WIRE_MUL
-#define LDPC_WIRE_MUL 0  // 1: PROD wire as (Rc - 1) / max(Rc, 1) (one more packed op per two edges)
-#endif
 #ifndef LDPC_MS_LAUNDER
 #define LDPC_MS_LAUNDER 1  // min-sum: scaled minima computed once per check (see check_update_ms6)
 #endif
@@ -697,20 +694,8 @@ __device__ __forceinline__ float2 v2c_wire2(float2 x) {
 //   min(R, 1) - min(1/R, 1)   (R >= 1: 1 - 1/R;  R < 1: R - 1)
 // with both terms clamped below at 2^-23 (|x| <= 23): two v_med3_f32, one
 // v_rcp_f32 in place of the v_exp_f32, one packed subtraction per two edges.
-#if LDPC_WIRE_MUL
-__device__ __forceinline__ float ratio_wire(float R) {
-    const float lo = __builtin_amdgcn_fmed3f(R, 0x1p-23f, 0x1p23f);
-    const float hi = __builtin_amdgcn_fmed3f(R, 1.0f, 0x1p23f);
-    return (lo - 1.0f) * __builtin_amdgcn_rcpf(hi);
-}
-__device__ __forceinline__ float2 ratio_wire2(float2 R) {
-    const float2 lo = make_float2(__builtin_amdgcn_fmed3f(R.x, 0x1p-23f, 0x1p23f),
-                                  __builtin_amdgcn_fmed3f(R.y, 0x1p-23f, 0x1p23f));
-    const float2 hi = make_float2(__builtin_amdgcn_fmed3f(R.x, 1.0f, 0x1p23f),
-                                  __builtin_amdgcn_fmed3f(R.y, 1.0f, 0x1p23f));
-    return (lo - make_float2(1.0f, 1.0f)) * make_float2(__builtin_amdgcn_rcpf(hi.x), __builtin_amdgcn_rcpf(hi.y));
-}
-#else
+// (The algebraically equal (Rc - 1) / max(Rc, 1) forms 1 - a ~ 1/R as a difference
+// of two numbers near 1 and loses it to rounding for large R.)
 __device__ __forceinline__ float ratio_wire(float R) {
     return __builtin_amdgcn_fmed3f(R, 0x1p-23f, 1.0f) -
            __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(R), 0x1p-23f, 1.0f);
@@ -722,7 +707,6 @@ __device__ __forceinline__ float2 ratio_wire2(float2 R) {
                                  __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(R.y), 0x1p-23f, 1.0f));
     return lo - u;
 }
-#endif
 
 // Check-node update over D messages in registers; entries i >= d are padding
 // (+inf for min-sum, unit factors for sum-product).  Same product / min order as
@@ -1042,7 +1026,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
         auto var_phase_prod = [&](auto final_tag) {
             constexpr bool FINAL = decltype(final_tag)::value;
             int errs = 0;
-            auto edges = [&](auto &cv, auto Ev, auto at_j, auto put_j) {
+            auto edges = [&](auto &cv, auto Ev, auto put_j) {
                 // cv[j]: ratios of this variable's edges; put_j(j, wire)
                 decltype(Ev) pre[DV];
                 pre[0] = Ev;
@@ -1055,7 +1039,6 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     put_j(j, pre[j] * suf);
                     if (j > 0) suf = suf * cv[j];
                 }
-                (void)at_j;
                 return pre[DV - 1] * cv[DV - 1];  // posterior ratio
             };
 #pragma unroll
@@ -1076,7 +1059,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                         s = s + make_float2(__builtin_amdgcn_logf(cv[j].x), __builtin_amdgcn_logf(cv[j].y));
                     if constexpr (!MC) { pr[i] = s.x; pr[i + 1] = s.y; }
                 } else {
-                    const float2 post = edges(cv, make_float2(L[i], L[i + 1]), 0, [&](int j, float2 R) {
+                    const float2 post = edges(cv, make_float2(L[i], L[i + 1]), [&](int j, float2 R) {
                         const float2 w = ratio_wire2(R);
                         at(a0[j]) = w.x;
                         at(a1[j]) = w.y;
@@ -1116,7 +1099,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     for (int j = 0; j < DV; ++j) s += __builtin_amdgcn_logf(cv[j]);
                     if constexpr (!MC) pr[i] = s;
                 } else {
-                    const float post = edges(cv, L[i], 0, [&](int j, float R) { at(a0[j]) = ratio_wire(R); });
+                    const float post = edges(cv, L[i], [&](int j, float R) { at(a0[j]) = ratio_wire(R); });
                     if constexpr (ET) {
 #pragma unroll
                         for (int j = 0; j < DV; ++j) hsb[a0[j] >> 2] = (uint8_t)(post < 1.0f);
