@@ -37,6 +37,9 @@ constexpr int kWave = 64;
 #ifndef LDPC_MS_LAUNDER
 #define LDPC_MS_LAUNDER 1  // min-sum: scaled minima computed once per check (see check_update_ms6)
 #endif
+#ifndef LDPC_ET_DELTA
+#define LDPC_ET_DELTA 1  // early stop: rewrite a variable's hard-decision bytes only when it changes
+#endif
 #ifndef LDPC_BEC_DEC_BITS
 #define LDPC_BEC_DEC_BITS 1  // batch BEC decode (B >= 64) on the bit-sliced kernel when its planes fit LDS
 #endif
@@ -1013,6 +1016,18 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 #pragma unroll
             for (int i = 0; i < VPT; ++i) L[i] = __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[i], -126.0f, 126.0f));
         }
+        // ET: a variable's hard-decision bytes are rewritten only when its decision
+        // changes (bit i of hb = the decision last written for lane i; hfirst makes
+        // the first variable phase of a codeword write them all)
+        uint32_t hb = 0u;
+        bool hfirst = true;
+        auto put_hard = [&](int i, bool h, const uint32_t(&ad)[DV]) {
+            if (!LDPC_ET_DELTA || hfirst || ((hb >> i) & 1u) != (uint32_t)h) {
+#pragma unroll
+                for (int j = 0; j < DV; ++j) hsb[ad[j] >> 2] = (uint8_t)h;
+            }
+            hb = (hb & ~(1u << i)) | ((uint32_t)h << i);
+        };
         auto llr_log2 = [&](int i) -> float {  // PROD: channel LLR of lane i, message units
             // log2(E) restores it to ~1e-7 absolute; a value clamped at staging
             // (|LLR| > 87 nats) is re-read from the input instead
@@ -1065,11 +1080,8 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                         at(a1[j]) = w.y;
                     });
                     if constexpr (ET) {
-#pragma unroll
-                        for (int j = 0; j < DV; ++j) {
-                            hsb[a0[j] >> 2] = (uint8_t)(post.x < 1.0f);
-                            hsb[a1[j] >> 2] = (uint8_t)(post.y < 1.0f);
-                        }
+                        put_hard(i, post.x < 1.0f, a0);
+                        put_hard(i + 1, post.y < 1.0f, a1);
                         if constexpr (!MC) {  // prod r_j (no E: cannot overflow); logged at the end
                             float2 pq = cv[0];
 #pragma unroll
@@ -1101,8 +1113,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                 } else {
                     const float post = edges(cv, L[i], [&](int j, float R) { at(a0[j]) = ratio_wire(R); });
                     if constexpr (ET) {
-#pragma unroll
-                        for (int j = 0; j < DV; ++j) hsb[a0[j] >> 2] = (uint8_t)(post < 1.0f);
+                        put_hard(i, post < 1.0f, a0);
                         if constexpr (!MC) {
                             float pq = cv[0];
 #pragma unroll
@@ -1146,11 +1157,8 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     if (FINAL || ET) { pr[i] = s.x; pr[i + 1] = s.y; }
                 }
                 if constexpr (ET) {
-#pragma unroll
-                    for (int j = 0; j < DV; ++j) {
-                        hsb[a0[j] >> 2] = (uint8_t)(s.x < 0.0f);
-                        hsb[a1[j] >> 2] = (uint8_t)(s.y < 0.0f);
-                    }
+                    put_hard(i, s.x < 0.0f, a0);
+                    put_hard(i + 1, s.y < 0.0f, a1);
                 }
                 if constexpr (MC) errs += ((a0[0] < 4u * (E + lpos0)) & (s.x < 0.0f)) + ((a1[0] < 4u * (E + lpos0)) & (s.y < 0.0f));
                 // LDPC_VAR_PAIRS pairs' gathers in flight per thread (VGPR budget of
@@ -1177,8 +1185,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     if (FINAL || ET) pr[i] = s;
                 }
                 if constexpr (ET) {
-#pragma unroll
-                    for (int j = 0; j < DV; ++j) hsb[a0[j] >> 2] = (uint8_t)(s < 0.0f);
+                    put_hard(i, s < 0.0f, a0);
                 }
                 if constexpr (MC) errs += (a0[0] < 4u * (E + lpos0)) & (s < 0.0f);
             }
@@ -1243,6 +1250,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                 if constexpr (PROD) errs = var_phase_prod(std::false_type{});
                 else errs = var_phase(std::false_type{});
             }
+            hfirst = false;
             if (MC) {
                 const int w = wave_sum(errs);
                 if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[it + 1], w);
