@@ -20,6 +20,6 @@ for p in sys.argv[1:]:
     for r in range(3):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(s)
-        assert L.ldpc_bp_decode_batch_dev(h, llr.data_ptr(), B, it, algo, ct.c_float(0.75 if algo else 1.0), 0, None, hard.data_ptr(), None, ct.c_void_p(s.cuda_stream)) == 0
+        assert L.ldpc_bp_decode_batch_dev(h, llr.data_ptr(), B, it, algo, ct.c_float(0.75 if algo else 1.0), int(os.environ.get("ET", "0")), None, hard.data_ptr(), None, ct.c_void_p(s.cuda_stream)) == 0
         b.record(s); torch.cuda.synchronize(); ts.append(a.elapsed_time(b))
     print(f"{p:36s} {min(ts):9.2f} ms  {B/min(ts)*1e3*it/100:10.1f} cw/s@100it  errs {int(hard.sum())}")
