@@ -549,11 +549,12 @@ int ldpc_bec_decode_batch_dev(const ldpc_graph *g, uint8_t *d_words, int B, int 
     return LDPC_OK;
 }
 
-static int bec_host(const ldpc_graph *g, uint8_t *words, int B, int max_iters, int32_t *errors, int32_t *its) {
+// Caller holds g_mu (the workspace and, for the drop-in, the cached graph stay valid).
+static int bec_host_locked(const ldpc_graph *g, uint8_t *words, int B, int max_iters, int32_t *errors,
+                           int32_t *its) {
     const size_t n = g->n;
     for (size_t i = 0; i < (size_t)B * n; ++i)
         LDPC_REQUIRE(words[i] <= 2, "channel word value outside {0, 1, 2}");
-    std::lock_guard<std::mutex> lk(g_mu);
     Workspace &ws = workspace(nullptr);
     LDPC_HIP(ws.words.ensure((size_t)B * n));
     LDPC_HIP(ws.errors.ensure(sizeof(int32_t) * (size_t)B * (max_iters > 0 ? max_iters : 1)));
@@ -571,6 +572,11 @@ static int bec_host(const ldpc_graph *g, uint8_t *words, int B, int max_iters, i
         LDPC_HIP(hipMemcpy(errors, de, sizeof(int32_t) * (size_t)B * max_iters, hipMemcpyDeviceToHost));
     LDPC_HIP(hipMemcpy(its, di, sizeof(int32_t) * (size_t)B, hipMemcpyDeviceToHost));
     return LDPC_OK;
+}
+
+static int bec_host(const ldpc_graph *g, uint8_t *words, int B, int max_iters, int32_t *errors, int32_t *its) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return bec_host_locked(g, words, B, max_iters, errors, its);
 }
 
 int ldpc_bec_decode_batch(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list, int n,
@@ -598,9 +604,10 @@ int message_passing(int *Mvc, int iterations, int *variable_to_check_list, int *
         LDPC_REQUIRE(Mvc[v] >= 0 && Mvc[v] <= 2, "Mvc value outside {0, 1, 2}");
         w[v] = (uint8_t)Mvc[v];
     }
-    ldpc_graph *g = nullptr;
+    // One lock across the cache lookup and the decode: another thread replacing the cached
+    // graph cannot free it while this call still uses it.
+    std::lock_guard<std::mutex> lk(g_mu);
     {
-        std::lock_guard<std::mutex> lk(g_mu);
         int dev = 0;
         (void)hipGetDevice(&dev);
         const size_t Ev = (size_t)n * dv, Ec = (size_t)(n - k) * dc;
@@ -617,10 +624,9 @@ int message_passing(int *Mvc, int iterations, int *variable_to_check_list, int *
             if (rc) return rc;
             c.n = n; c.k = k; c.dv = dv; c.dc = dc; c.dev = dev; c.hash = h;
         }
-        g = c.g;
     }
     int32_t it = 0;
-    rc = bec_host(g, w.data(), 1, iterations, errors, &it);
+    rc = bec_host_locked(g_dropin.g, w.data(), 1, iterations, errors, &it);
     if (rc) return rc;
     for (int v = 0; v < n; ++v) Mvc[v] = w[v];
     return it;

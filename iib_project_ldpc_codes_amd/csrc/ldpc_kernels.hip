@@ -911,6 +911,7 @@ struct BpArgs {
 template <int DV, int DC, int T, int VPT, int ALGO, bool ET, bool MC>
 __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
     static_assert(DC % 2 == 0, "pair layout: the ET parity reads whole words");
+    static_assert(!ET || VPT <= 32, "early stop keeps one decision bit per lane in a 32-bit mask");
     extern __shared__ __align__(16) unsigned char smem[];
     float *msg = reinterpret_cast<float *>(smem);
     const int Ep = a.E + kLdsDummy;  // a.E = lds_pair_span(m, DC)

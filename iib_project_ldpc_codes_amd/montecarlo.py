@@ -7,8 +7,14 @@ rule (parallel_simulator.py:198) and accumulates int64 counters on the device.
 
 Multi-GPU (one process per GPU, torch.distributed): trials shard by index --
 rank r of W runs the batch of trials [(round*W + r)*B, +B); the only collective
-is one all-reduce of the counter vector per round (RCCL over xGMI with backend
-"nccl", gloo on CPU), used for the global stop rule and the final result.
+is one all-reduce per round of [counter deltas | per-rank frame errors | time
+flag] (RCCL over xGMI with backend "nccl", gloo on CPU).  The stop rule is the
+reference's sequential one in global trial order: in the round that crosses
+stop_frame_errors, ranks before the crossing keep their whole batch, the
+crossing rank re-runs its batch (Philox streams are keyed by trial index, so
+the re-run is identical) with the in-batch cut at its share of the remaining
+frame errors, and later ranks drop theirs -- the counters then equal one
+process's `while block_error < 200 and i < num_tests` loop exactly.
 """
 import time
 
@@ -142,24 +148,91 @@ class MonteCarlo:
             self.dist.all_reduce(c, group=self.pg)
         return c.cpu().numpy()
 
+    def _frames_trials(self, c, c_ml):
+        """(frame errors, trials) the stop rules count: BP counters, or ML ones when
+        message passing is off (parallel_simulator.py:226-231 / :240-241)."""
+        src = c if self.message_passing else c_ml
+        return int(src[1]), int(src[0])
+
+    def _run_delta(self, first_cw, B, stop):
+        """Run one batch into fresh zero counters; return (delta, delta_ml)."""
+        saved = self.counters, self.counters_ml
+        self.counters = self.torch.zeros_like(saved[0])
+        self.counters_ml = None if saved[1] is None else self.torch.zeros_like(saved[1])
+        try:
+            if B > 0:
+                self.run_batch(first_cw, B, stop)
+            return self.counters, self.counters_ml
+        finally:
+            self.counters, self.counters_ml = saved
+
+    def _add(self, delta):
+        self.counters += delta[0]
+        if delta[1] is not None:
+            self.counters_ml += delta[1]
+
+    def _allreduce(self, vec):
+        if self.dist.get_backend(self.pg) == "gloo":
+            vec = vec.cpu()
+        self.dist.all_reduce(vec, group=self.pg)
+        return vec.cpu().numpy()
+
+    def _batch_size(self, num_tests, trials_before, slot):
+        """Trials this rank runs in the round: the reference stops at exactly num_tests
+        (parallel_simulator.py:198), so the round's last batches are clamped in trial order."""
+        if not num_tests:
+            return self.batch
+        return int(max(0, min(self.batch, num_tests - trials_before - slot * self.batch)))
+
     def run(self, num_tests, stop_frame_errors=200, time_limit=None):
         """Run rounds until the global counters reach stop_frame_errors frame errors or
-        num_tests trials, or time_limit seconds pass (parallel_simulator.py:198)."""
+        num_tests trials, or time_limit seconds pass (parallel_simulator.py:198).  Counts
+        equal one sequential process's over the same trials; the time limit is decided
+        collectively (every rank leaves on the same round)."""
         t0 = time.time()
+        g = self._global()
+        nc = len(self.counters)
+        frames, trials = self._frames_trials(g[:nc], g[nc:])
         while True:
-            first_cw = (self.rounds * self.world + self.rank) * self.batch
-            # one process: the exact sequential stop happens inside the batch
-            stop = stop_frame_errors if self.world == 1 else 0
-            self.run_batch(first_cw, self.batch, stop)
-            self.rounds += 1
-            g = self._global()
-            frames = g[1] if self.message_passing else g[len(self.counters) + 1]
             if stop_frame_errors and frames >= stop_frame_errors:
                 break
-            trials = g[0] if self.message_passing else g[len(self.counters)]
             if num_tests and trials >= num_tests:
                 break
-            if time_limit is not None and time.time() - t0 > time_limit:
+            first_cw = (self.rounds * self.world + self.rank) * self.batch
+            B = self._batch_size(num_tests, trials, self.rank)
+            if self.world == 1:
+                # one process: the exact sequential stop happens inside the batch
+                self.run_batch(first_cw, B, stop_frame_errors)
+                self.rounds += 1
+                g = self._global()
+                expired = time_limit is not None and time.time() - t0 > time_limit
+            else:
+                delta = self._run_delta(first_cw, B, 0)
+                f_mine = self._frames_trials(*[None if d is None else d.cpu() for d in delta])[0]
+                onehot = self.torch.zeros(self.world + 1, dtype=self.torch.int64, device=self.device)
+                onehot[self.rank] = f_mine
+                onehot[self.world] = int(time_limit is not None and time.time() - t0 > time_limit)
+                parts = [delta[0]] + ([delta[1]] if delta[1] is not None else []) + [onehot]
+                red = self._allreduce(self.torch.cat(parts))
+                per_rank = red[-(self.world + 1):-1]
+                expired = bool(red[-1])
+                if stop_frame_errors and frames + int(per_rank.sum()) >= stop_frame_errors:
+                    quota = stop_frame_errors - frames - int(per_rank[:self.rank].sum())
+                    if quota <= 0:
+                        delta = (self.torch.zeros_like(delta[0]),
+                                 None if delta[1] is None else self.torch.zeros_like(delta[1]))
+                    elif quota <= f_mine:
+                        # the crossing rank: cut at its share, in trial order
+                        delta = self._run_delta(first_cw, B, quota)
+                    self._add(delta)
+                    self.rounds += 1
+                    g = self._global()
+                    break
+                self._add(delta)
+                self.rounds += 1
+                g = g + red[:len(red) - (self.world + 1)]
+            frames, trials = self._frames_trials(g[:nc], g[nc:])
+            if expired:
                 break
         return self.results(g)
 

@@ -56,6 +56,8 @@ def lib():
         _lib.oracle_sample_regular_batch.restype = None
         _lib.oracle_sample_csr.argtypes = [i, i, P, P, u64, u64, i, P, P]
         _lib.oracle_sample_csr.restype = i
+        _lib.oracle_check_update.argtypes = [P, i, i, f]
+        _lib.oracle_check_update.restype = None
         _lib.oracle_num_threads.argtypes = []
         _lib.oracle_num_threads.restype = i
     return _lib
@@ -116,6 +118,13 @@ def bp_decode_batch(csr, llr, max_iters, algo=0, alpha=1.0, early_stop=False):
     lib().oracle_bp_decode_batch(_p(cptr), _p(cvar), _p(vptr), _p(vslot), n, m, _p(llr), B, max_iters,
                                  algo, alpha, int(bool(early_stop)), _p(post), _p(hard), _p(its))
     return post, hard, its
+
+
+def check_update(x, algo=0, alpha=1.0):
+    """One check-node update (the decoders' rule) on a copy of the d inputs x."""
+    x = np.ascontiguousarray(x, dtype=np.float32).copy()
+    lib().oracle_check_update(_p(x), x.shape[0], algo, alpha)
+    return x
 
 
 def num_threads():

@@ -1,0 +1,111 @@
+"""GPU parity at the benchmark and configs[4] sizes (BASELINE.json configs[1] and [4]).
+
+* Headline (bench.py's step): (3,6) n = 10,000 code `random_regular(10000, 3, 6, seed=1)`,
+  BI-AWGN sigma = 0.85 frames of the bench's own 65,536-frame batch (Philox seed 2026),
+  fp32 sum-product, exactly 50 iterations.  The GPU decodes the whole batch in one launch
+  (the timed kernel, persistent grid); 2,048 frames spread over the batch are decoded by
+  the oracle.  Tolerances (stated):
+    - >= 99 % of frames have identical hard decisions (frames whose BP does not converge
+      can follow ulp-separated trajectories: the kernel's hardware rcp / exp2 / log2 vs libm);
+    - FER of the two decoders on the same frames within the 3-sigma binomial interval;
+    - posteriors of frames with identical decisions: |d| <= POST_ATOL + POST_RTOL |post_cpu|
+      for >= 99.9 % of values, all within SAT_ATOL + SAT_RTOL |post_cpu| (50 iterations of
+      saturated messages: the check rule's D - N cancellation, see test_oracle_golden.py).
+* configs[4] (parallel_simulator_expurgated.py:169-285): the fused ensemble Monte-Carlo
+  (a fresh device-sampled (3,6) n = 64,800 graph per trial, BEC channel, 200 iterations,
+  expurgation X = 3) against the oracle's sampler restatement + message_passing
+  restatement, trial by trial: counters bit-exact.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+POST_ATOL, POST_RTOL = 1e-3, 1e-3
+SAT_ATOL, SAT_RTOL = 2e-2, 1e-2
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    assert t.cuda.is_available(), "GPU tests need a visible MI355X"
+    return t
+
+
+def _dump(name, stats):
+    d = os.environ.get("LDPC_PARITY_DUMP")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name + ".json"), "w") as f:
+            json.dump(stats, f, indent=1)
+    print(name, json.dumps(stats))
+
+
+def test_headline_bench_config_spa_vs_oracle(torch):
+    import bench
+    from iib_project_ldpc_codes_amd import decoder
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = TannerGraph.random_regular(bench.N_BITS, bench.DV, bench.DC, seed=1)  # the bench code
+    B = bench.BATCH
+    llr = decoder.channel_dev("awgn", bench.SIGMA, 2026, 0, g.n, B)  # the bench batch (rank 0)
+    post, hard, its = decoder.bp_decode_dev(g, llr, bench.ITERS, "spa", early_stop=False)
+    torch.cuda.synchronize()
+    assert g.kernel_name() == "bp_lds_kernel<3,6>"
+    assert int(its.min().item()) == bench.ITERS
+    pick = np.arange(0, B, B // 2048)
+    idx = torch.from_numpy(pick).cuda()
+    gp, gh = post[idx].cpu().numpy(), hard[idx].cpu().numpy()
+    csr = oracle.csr_from_lists(g.variable_lookup, g.check_lookup, g.n, g.m, bench.DV, bench.DC)
+    op, oh, _ = oracle.bp_decode_batch(csr, llr[idx].cpu().numpy(), bench.ITERS, 0)
+    same = np.all(gh == oh, axis=1)
+    fer_g, fer_o = float(gh.any(axis=1).mean()), float(oh.any(axis=1).mean())
+    F = len(pick)
+    band = 3 * np.sqrt(max(fer_o * (1 - fer_o), 1.0 / F) / F)
+    d = np.abs(gp[same].astype(np.float64) - op[same])
+    ref = np.abs(op[same].astype(np.float64))
+    close = d <= POST_ATOL + POST_RTOL * ref
+    stats = {"frames": F, "identical_frames": float(same.mean()), "fer_gpu": fer_g, "fer_oracle": fer_o,
+             "fer_band_3sigma": band, "post_close_frac": float(close.mean()),
+             "post_max_abs": float(d.max()), "post_max_rel": float((d / np.maximum(ref, 1.0)).max()),
+             "post_abs_max_cpu": float(ref.max()),
+             "failing_frames_identical": float(same[oh.any(axis=1)].mean()) if oh.any() else None,
+             "fer_full_batch_gpu": float(hard.any(dim=1).float().mean().item())}
+    _dump("headline_parity", stats)
+    assert same.mean() >= 0.99, stats
+    assert abs(fer_g - fer_o) <= band, stats
+    assert close.mean() >= 0.999, stats
+    assert np.all(d <= SAT_ATOL + SAT_RTOL * ref), stats
+
+
+def test_cfg5_ensemble_mc_n64800_vs_oracle(torch):
+    """configs[4]: 64 trials on 64 fresh n = 64,800 graphs, 200 iterations, X = 3, run as
+    two 32-trial batches (trial index = graph index = channel subsequence)."""
+    from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
+    n, iters, eps, seed, X, B = 64800, 200, 0.425, 23, 3, 32
+    mc = MonteCarlo.ensemble(n, 3, 6, "bec", eps, iters, seed=seed, batch=B, expurgation=X)
+    mc.run_batch(0, B)
+    mc.run_batch(B, B)
+    torch.cuda.synchronize()
+    got = mc.counters.cpu().numpy()
+    T = 2 * B
+    chk, var, _ = oracle.sample_regular_batch(n, 3, 6, seed, 0, T)
+    words = oracle.channel(oracle.CH_BEC, eps, seed, 0, n, T)
+    want = np.zeros(4 + iters + 1, np.int64)
+    for t in range(T):
+        _, err, it = oracle.message_passing(words[t], iters, var[t], chk[t], n, n // 2, 3, 6)
+        curve = np.insert(err, 0, int(np.count_nonzero(words[t] == 2)))
+        if curve[-1] > X:  # parallel_simulator_expurgated.py:238
+            want[4:] += curve
+            want[1] += curve[-1] != 0
+            want[2] += curve[-1]
+        want[0] += 1
+        want[3] += it
+    _dump("cfg5_ensemble_mc", {"trials": int(want[0]), "frame_errors": int(want[1]),
+                               "mean_iterations": float(want[3] / want[0])})
+    assert 0 < want[1] < T  # both decoded and failed trials at eps = 0.425 (threshold 0.4294)
+    np.testing.assert_array_equal(got, want)

@@ -6,6 +6,7 @@ stop rule -- independently of the GPU kernels (which tests/test_gpu_parity.py pi
 same oracle counters)."""
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -18,7 +19,10 @@ from oracle import oracle
 N, ITERS, B, EPS, SEED = 200, 20, 32, 0.42, 11
 
 
-def oracle_batch_counters(g, first_cw, Bn, iters, X=-1):
+def oracle_batch_counters(g, first_cw, Bn, iters, X=-1, remaining=0):
+    """Counters of trials first_cw.. on the oracle; remaining > 0 applies the sequential
+    stop (parallel_simulator.py:198): keep trials up to the one that brings the frame
+    errors to `remaining`."""
     words = oracle.channel(oracle.CH_BEC, EPS, SEED, first_cw, g.n, Bn)
     _, err, its = oracle.bec_decode_batch(words, iters, g.variable_lookup, g.check_lookup, g.n, g.k, g.dv, g.dc)
     c = np.zeros(4 + iters + 1, np.int64)
@@ -30,6 +34,8 @@ def oracle_batch_counters(g, first_cw, Bn, iters, X=-1):
             c[2] += curve[-1]
         c[0] += 1
         c[3] += its[b]
+        if remaining and c[1] >= remaining:
+            break
     return c
 
 
@@ -41,7 +47,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, num_tests, q):
+def _worker(rank, world, port, num_tests, stop_frames, time_limit, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -51,40 +57,85 @@ def _worker(rank, world, port, num_tests, q):
         seen = []
 
         def executor(first_cw, Bn, stop, counters):
-            seen.append(first_cw)
-            counters += torch.from_numpy(oracle_batch_counters(g, first_cw, Bn, ITERS))
+            # the device executor's contract: the in-batch cut counts from counters[1]
+            seen.append((first_cw, Bn, stop))
+            rem = int(stop - counters[1]) if stop else 0
+            if stop and rem <= 0:
+                return
+            counters += torch.from_numpy(oracle_batch_counters(g, first_cw, Bn, ITERS, remaining=rem))
+            if time_limit is not None and rank == world - 1:
+                time.sleep(0.05)  # this rank's clock runs out later than rank 0's
 
         mc = MonteCarlo(g, "bec", EPS, ITERS, seed=SEED, batch=B, executor=executor)
-        res = mc.run(num_tests=num_tests, stop_frame_errors=10 ** 9)
+        res = mc.run(num_tests=num_tests, stop_frame_errors=stop_frames, time_limit=time_limit)
         q.put((rank, seen, res["raw_counters"].tolist(), mc.rounds))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_sharded_mc_matches_single_process(world):
+def _spawn(target, world, *args):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    num_tests = 5 * B
-    procs = [ctx.Process(target=_worker, args=(r, world, port, num_tests, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    out.sort()
+    return sorted(out, key=lambda o: o[0])
+
+
+def sequential_counters(g, num_tests, stop_frames):
+    """One process, trial by trial: `while block_error < stop and i < num_tests`."""
+    T = num_tests if num_tests else 64 * B
+    return oracle_batch_counters(g, 0, T, ITERS, remaining=stop_frames)
+
+
+@pytest.mark.parametrize("world,num_tests", [(2, 5 * B), (2, 5 * B + 7), (3, 4 * B + 5)])
+def test_sharded_mc_matches_single_process(world, num_tests):
+    """No frame-error stop: exactly num_tests trials (the last round clamped in trial order)."""
+    out = _spawn(_worker, world, num_tests, 0, None)
     rounds = out[0][3]
     assert all(o[3] == rounds for o in out)
-    # rank r ran batches (round*W + r)*B: disjoint, covering [0, rounds*W*B)
-    starts = sorted(s for o in out for s in o[1])
-    assert starts == [i * B for i in range(rounds * world)]
-    assert rounds * world * B >= num_tests
-    # both ranks see the same global counters == one process over the same trials
+    # rank r ran batches (round*W + r)*B: disjoint, covering [0, num_tests)
+    runs = sorted((s, n) for o in out for s, n, _ in o[1] if n > 0)
+    assert [s for s, _ in runs] == [i * B for i in range(len(runs))]
+    assert sum(n for _, n in runs) == num_tests
     from iib_project_ldpc_codes_amd.graph import TannerGraph
     g = TannerGraph.random_regular(N, 3, 6, seed=5)
-    want = oracle_batch_counters(g, 0, rounds * world * B, ITERS)
+    want = oracle_batch_counters(g, 0, num_tests, ITERS)
+    for o in out:
+        np.testing.assert_array_equal(np.array(o[2]), want)
+
+
+@pytest.mark.parametrize("world,stop", [(2, 5), (2, 17), (3, 11), (4, 40)])
+def test_sharded_stop_rule_is_sequential(world, stop):
+    """The global frame-error stop cuts at exactly the same trial as one process
+    (parallel_simulator.py:198), whichever rank's batch holds the crossing."""
+    out = _spawn(_worker, world, 0, stop, None)
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = TannerGraph.random_regular(N, 3, 6, seed=5)
+    want = sequential_counters(g, 0, stop)
+    assert want[1] == stop
+    for o in out:
+        np.testing.assert_array_equal(np.array(o[2]), want)
+    assert len({o[3] for o in out}) == 1
+
+
+def test_sharded_time_limit_is_collective():
+    """A time limit ends every rank on the same round (no rank left waiting in an
+    all-reduce), and the counters are the trials of the rounds run."""
+    world = 2
+    out = _spawn(_worker, world, 0, 0, 0.12)
+    rounds = {o[3] for o in out}
+    assert len(rounds) == 1
+    r = rounds.pop()
+    assert r >= 1
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = TannerGraph.random_regular(N, 3, 6, seed=5)
+    want = oracle_batch_counters(g, 0, r * world * B, ITERS)
     for o in out:
         np.testing.assert_array_equal(np.array(o[2]), want)
 
@@ -121,23 +172,14 @@ def test_sharded_ml_mc_matches_single_process():
     """Optimal (ML-only) mode: the ML counters are all-reduced with the others and the
     trial-count stop uses them (message_passing=False)."""
     world = 2
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
     num_tests = 3 * B
-    procs = [ctx.Process(target=_worker_ml, args=(r, world, port, num_tests, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    out = [q.get(timeout=300) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    out = _spawn(_worker_ml, world, num_tests)
     rounds = out[0][4]
-    assert all(o[4] == rounds for o in out) and rounds * world * B >= num_tests
+    assert all(o[4] == rounds for o in out)
     from iib_project_ldpc_codes_amd.graph import TannerGraph
     g = TannerGraph.random_regular(N, 3, 6, seed=5)
     cptr, cvar, _, _ = g.to_csr()
-    T = rounds * world * B
+    T = num_tests
     words = oracle.channel(oracle.CH_BEC, EPS, SEED, 0, g.n, T).astype(np.uint8)
     _, uns = oracle.ml_decode_batch(cptr, cvar, words, g.n, g.m)
     for o in out:

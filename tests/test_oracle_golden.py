@@ -79,3 +79,75 @@ def test_oracle_fixed_code_fer_ber_near_reference_probe():
     fer, ber = float((final > 0).mean()), float(final.sum() / (T * n))
     assert abs(fer - 0.0905) < 0.015, fer
     assert abs(ber - 0.0213) < 0.004, ber
+
+
+# ------------------------------------------------ soft check rules vs float64
+XMAX64 = 23 * np.log(2.0)  # the rules' saturation: |x| is clamped at 23 ln 2 (e^-|x| >= 2^-23)
+
+
+def _spa_float64(x):
+    """Textbook tanh rule in float64: c_j = 2 atanh(prod_{i != j} tanh(x_i / 2)), inputs
+    saturated at XMAX64 like the decoders -- independent of the oracle's ratio form."""
+    x = np.asarray(x, np.float64)
+    t = np.tanh(np.minimum(np.abs(x), XMAX64) / 2) * np.where(x < 0, -1.0, 1.0)
+    return np.array([2 * np.arctanh(np.prod(np.delete(t, j))) for j in range(len(x))])
+
+
+def _minsum_float64(x, alpha):
+    x = np.asarray(x, np.float32)
+    out = np.empty_like(x)
+    for j in range(len(x)):
+        rest = np.delete(x, j)
+        sign = -1.0 if (np.count_nonzero(rest < 0) % 2) else 1.0
+        out[j] = np.float32(sign * float(alpha) * float(np.min(np.abs(rest))))  # one fp32 rounding
+    return out
+
+
+def test_oracle_spa_rule_vs_float64_tanh():
+    """The oracle's fp32 sum-product check rule (ratio form, the definition the GPU kernels
+    are held to) against the float64 tanh / atanh rule, over degrees 2-8 and input scales
+    from 0.1 to 60 nats (saturated inputs included).  Tolerance: the ratio form's output is
+    ln((D+N)/(D-N)); fp32 rounding of D +- N (|D| <= 1) is amplified by D/(D-N) ~ e^|c|/2,
+    so |c32 - c64| <= 2 d 2^-24 e^|c64| + 4e-6 |c64| -- a few 1e-7 for |c| < 3, ~0.3 at the
+    saturation |c| ~ 15.6 nats, where any fp32 formulation is that coarse."""
+    rng = np.random.default_rng(7)
+    worst = 0.0
+    for _ in range(6000):
+        d = int(rng.integers(2, 9))
+        scale = rng.choice([0.1, 0.5, 2.0, 5.0, 20.0, 60.0])
+        x = (rng.normal(size=d) * scale).astype(np.float32)
+        if rng.random() < 0.1:
+            x[rng.integers(d)] = np.float32(0.0)
+        got = oracle.check_update(x, 0).astype(np.float64)
+        want = _spa_float64(x)
+        tol = 2 * d * 2.0 ** -24 * np.exp(np.abs(want)) + 4e-6 * np.abs(want)
+        worst = max(worst, float(np.max(np.abs(got - want) / np.maximum(tol, 1e-30))))
+        assert np.all(np.abs(got - want) <= tol), (x, got, want)
+    assert worst > 0.05  # the bound is not vacuous
+
+
+def test_oracle_spa_rule_unsaturated_precision():
+    """Away from saturation (all |x| <= 6 nats) the rule is fp32-accurate: relative error
+    <= 2e-5 + absolute 1e-6."""
+    rng = np.random.default_rng(8)
+    for _ in range(3000):
+        d = int(rng.integers(2, 9))
+        x = rng.uniform(-6, 6, size=d).astype(np.float32)
+        got = oracle.check_update(x, 0).astype(np.float64)
+        np.testing.assert_allclose(got, _spa_float64(x), rtol=2e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("alpha", [1.0, 0.75, 0.8125])
+def test_oracle_minsum_rule_vs_float64(alpha):
+    """Normalized min-sum: c_j = alpha * min_{i != j} |x_i| * prod_{i != j} sign(x_i), with
+    one fp32 rounding of the product -- bit-exact, incl. ties, zeros and huge inputs."""
+    rng = np.random.default_rng(9)
+    for _ in range(3000):
+        d = int(rng.integers(2, 9))
+        x = (rng.normal(size=d) * rng.choice([0.5, 5.0, 1e30])).astype(np.float32)
+        if rng.random() < 0.2:
+            x[rng.integers(d)] = x[rng.integers(d)]  # ties
+        if rng.random() < 0.1:
+            x[rng.integers(d)] = np.float32(0.0)
+        got = oracle.check_update(x, 1, alpha)
+        np.testing.assert_array_equal(got, _minsum_float64(x, alpha))
