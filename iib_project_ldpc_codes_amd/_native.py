@@ -75,6 +75,8 @@ def lib():
         "ldpc_ml_decode_batch": ([P, P, i, P, P], i),
         "ldpc_ml_ensemble_decode_dev": ([i, i, i, P, P, i, P, P, P], i),
         "ldpc_mc_ml_batch_dev": ([P, i, i, i, f, u64, u64, i, i, i, i, i64, P, P, P], i),
+        "ldpc_mc_run": ([P, P, i, i, i, i, i, f, i, f, i, u64, i, i, i64, i64, i, ct.c_double, P, i, P, P], i),
+        "ldpc_mc_run_csr": ([P, P, P, P, i, i, i, f, i, f, i, u64, i, i, i64, i64, i, ct.c_double, P, i, P, P], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -101,4 +103,5 @@ def exported_symbols():
             "ldpc_bp_decode_batch_dev", "ldpc_channel_dev", "ldpc_mc_batch_dev", "ldpc_last_error",
             "ldpc_device_count", "ldpc_set_device", "ldpc_sync", "ldpc_debug_lane_layout", "ldpc_debug_irr_layout", "ldpc_bp_kernel_name", "ldpc_sample_regular_dev",
             "ldpc_sample_regular", "ldpc_mc_ensemble_batch_dev", "ldpc_ml_decode_batch_dev", "ldpc_ml_decode_batch",
-            "ldpc_ml_ensemble_decode_dev", "ldpc_mc_ml_batch_dev", "ldpc_sample_csr_dev", "ldpc_sample_csr"]
+            "ldpc_ml_ensemble_decode_dev", "ldpc_mc_ml_batch_dev", "ldpc_sample_csr_dev", "ldpc_sample_csr",
+            "ldpc_mc_run", "ldpc_mc_run_csr"]

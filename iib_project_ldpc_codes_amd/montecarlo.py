@@ -262,3 +262,45 @@ class MonteCarlo:
             "error_curve": curve / (n * trials) if trials else curve,
             "raw_counters": g,
         }
+
+
+def mc_run(graph, channel, param, max_iters, devices=(0,), num_tests=0, stop_frame_errors=200, algo="spa",
+           alpha=1.0, early_stop=True, expurgation=-1, seed=0, batch=4096, time_limit=None):
+    """A whole run over several devices of THIS process through the C ABI's ldpc_mc_run
+    (one RCCL all-reduce per round, exact sequential stop rule; no torch.distributed).
+    graph: a TannerGraph (fixed code; irregular graphs go through ldpc_mc_run_csr) or
+    ``("ensemble", n, dv, dc)`` for a fresh code per trial.  Returns the same dict as
+    MonteCarlo.results."""
+    import ctypes as ct
+    L = _native.lib()
+    C = _native.MC_NCOUNT + int(max_iters) + 1
+    counters = np.zeros(C, np.int64)
+    rounds = np.zeros(1, np.int64)
+    devs = np.ascontiguousarray(devices, dtype=np.int32)
+    common = (CHANNELS[channel], float(param), ALGOS[algo], float(alpha), int(bool(early_stop)), int(seed),
+              int(max_iters), int(expurgation), int(num_tests or 0), int(stop_frame_errors or 0), int(batch),
+              float(time_limit or 0.0), devs.ctypes.data, len(devs), counters.ctypes.data, rounds.ctypes.data)
+    if isinstance(graph, tuple) and graph[0] == "ensemble":
+        _, n, dv, dc = graph
+        rc = L.ldpc_mc_run(None, None, n, n - n * dv // dc, dv, dc, *common)
+        name = "ldpc_mc_run"
+    elif graph.csr is None:
+        v2c = np.ascontiguousarray(graph.variable_lookup, np.int32)
+        c2v = np.ascontiguousarray(graph.check_lookup, np.int32)
+        n = graph.n
+        rc = L.ldpc_mc_run(v2c.ctypes.data, c2v.ctypes.data, graph.n, graph.k, graph.dv, graph.dc, *common)
+        name = "ldpc_mc_run"
+    else:
+        cptr, cvar, vptr, vslot = [np.ascontiguousarray(a, np.int32) for a in graph.to_csr()]
+        n = graph.n
+        rc = L.ldpc_mc_run_csr(cptr.ctypes.data, cvar.ctypes.data, vptr.ctypes.data, vslot.ctypes.data, graph.n,
+                               graph.m, *common)
+        name = "ldpc_mc_run_csr"
+    _native.check(rc, name)
+    trials = int(counters[0])
+    curve = counters[_native.MC_NCOUNT:].astype(np.float64)
+    return {"num_tests": trials, "frame_errors": int(counters[1]), "bit_errors": int(counters[2]),
+            "iterations": int(counters[3]), "fer": counters[1] / trials if trials else float("nan"),
+            "ber": counters[2] / (trials * n) if trials else float("nan"),
+            "error_curve": curve / (n * trials) if trials else curve, "raw_counters": counters,
+            "rounds": int(rounds[0]), "devices": [int(d) for d in devs]}

@@ -149,6 +149,39 @@ int ldpc_mc_batch_dev(const ldpc_graph *g, int channel, float param, uint64_t se
                       int64_t stop_frame_errors, int64_t *d_counters, void *stream);
 
 /* ---------------------------------------------------------------------- */
+/* Whole Monte-Carlo run over several devices of one process */
+/* ---------------------------------------------------------------------- */
+/*
+ * Replaces the trial loop of run_simulation / run_simulation_fixed_ldpc
+ * (parallel_simulator.py:198-244, :354-379; parallel_simulator_expurgated.py
+ * :200-256) together with the reference's multi-process fan-out
+ * (parallel_simulator.py:403-445) and CSV merge (tools/combine_data.py:64-95):
+ * one call runs `while frame_errors < stop_frame_errors and trials < num_tests`
+ * (either limit <= 0 = none; time_limit_s <= 0 = none, else checked after each
+ * round) over devices[0..ndev) (HIP ordinals, each listed once).  Device slot r
+ * of round R decodes trials [(R*ndev + r)*batch, +batch); the counters of each
+ * round are summed with ONE ncclAllReduce over the devices (RCCL,
+ * ncclCommInitAll, loaded from librccl.so.1 at first use).  The stop rule is
+ * applied exactly in global trial order, so the result equals one sequential
+ * process over the same trials whatever ndev is.
+ *   Graph: the reference's edge lists (fixed code, built on every device) -- or
+ *   both lists NULL for ensemble mode (a fresh random (dv, dc) code per trial,
+ *   BEC only, parallel_simulator.py:215); ldpc_mc_run_csr takes a CSR graph
+ *   (irregular codes).
+ *   counters (host) int64[LDPC_MC_NCOUNT + max_iters + 1], layout as
+ *   ldpc_mc_batch_dev, overwritten; rounds (may be NULL) = rounds run.
+ */
+int ldpc_mc_run(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list, int n, int k,
+                int dv, int dc, int channel, float param, int algo, float alpha, int early_stop, uint64_t seed,
+                int max_iters, int expurgation, int64_t num_tests, int64_t stop_frame_errors, int batch,
+                double time_limit_s, const int *devices, int ndev, int64_t *counters, int64_t *rounds);
+int ldpc_mc_run_csr(const int32_t *check_ptr, const int32_t *check_var, const int32_t *var_ptr,
+                    const int32_t *var_slot, int n, int m, int channel, float param, int algo, float alpha,
+                    int early_stop, uint64_t seed, int max_iters, int expurgation, int64_t num_tests,
+                    int64_t stop_frame_errors, int batch, double time_limit_s, const int *devices, int ndev,
+                    int64_t *counters, int64_t *rounds);
+
+/* ---------------------------------------------------------------------- */
 /* Random regular graphs + ensemble Monte-Carlo           */
 /* ---------------------------------------------------------------------- */
 /*

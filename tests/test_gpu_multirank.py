@@ -72,3 +72,43 @@ def test_two_ranks_equal_sequential(case):
         assert p.exitcode == 0
     for rank, counters, rounds in out:
         np.testing.assert_array_equal(np.array(counters), want, err_msg=f"rank {rank}")
+
+
+# ------------------------------------------- ldpc_mc_run (one process, RCCL over devices)
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_mc_run_one_device_equals_montecarlo(case):
+    """ldpc_mc_run through ctypes on device 0 (RCCL communicator of one rank): same
+    counters as montecarlo.MonteCarlo's sequential run, stop rule inside a batch."""
+    from iib_project_ldpc_codes_amd import montecarlo
+    c = CASES[case]
+    ref = _mc(case)
+    want = ref.run(num_tests=0, stop_frame_errors=STOP)["raw_counters"]
+    got = montecarlo.mc_run(ref.graph, c["channel"], c["param"], c["iters"], devices=(0,), num_tests=0,
+                            stop_frame_errors=STOP, algo=c["algo"], alpha=ref.alpha, early_stop=c["early_stop"],
+                            seed=SEED, batch=c["batch"])
+    np.testing.assert_array_equal(got["raw_counters"], want)
+    assert got["rounds"] == ref.rounds
+
+
+def test_mc_run_num_tests_clamp_and_ensemble():
+    """num_tests is met exactly (last batch clamped) -- fixed code and ensemble mode."""
+    import torch
+    from iib_project_ldpc_codes_amd import montecarlo
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
+    g = TannerGraph.random_regular(1000, 3, 6, seed=4)
+    got = montecarlo.mc_run(g, "bec", 0.42, 40, devices=(0,), num_tests=1000, stop_frame_errors=0, seed=3,
+                            batch=256)
+    ref = MonteCarlo(g, "bec", 0.42, 40, seed=3, batch=256)
+    for first, B in ((0, 256), (256, 256), (512, 256), (768, 232)):
+        ref.run_batch(first, B)
+    torch.cuda.synchronize()
+    assert got["num_tests"] == 1000
+    np.testing.assert_array_equal(got["raw_counters"], ref.counters.cpu().numpy())
+    ens = montecarlo.mc_run(("ensemble", 200, 3, 6), "bec", 0.40, 20, devices=(0,), num_tests=150,
+                            stop_frame_errors=0, seed=17, batch=96, expurgation=1)
+    mce = MonteCarlo.ensemble(200, 3, 6, "bec", 0.40, 20, seed=17, batch=96, expurgation=1)
+    mce.run_batch(0, 96)
+    mce.run_batch(96, 54)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(ens["raw_counters"], mce.counters.cpu().numpy())

@@ -47,6 +47,20 @@ def test_no_gpu_fails_loudly():
     assert "no HIP device" in _native.last_error()
 
 
+@pytest.mark.skipif(_torch_has_gpu(), reason="checks the no-GPU failure mode")
+def test_mc_run_no_gpu_fails_loudly():
+    """The multi-device run entry point has no CPU path either."""
+    from iib_project_ldpc_codes_amd import montecarlo, _native
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    g = TannerGraph.random_regular(120, 3, 6, seed=1)
+    with pytest.raises(_native.LdpcError) as e:
+        montecarlo.mc_run(g, "bec", 0.4, 20, devices=(0,), num_tests=64, batch=32)
+    assert e.value.rc == _native.LDPC_ENODEV
+    with pytest.raises(_native.LdpcError) as e:
+        montecarlo.mc_run(g, "bec", 0.4, 20, devices=(), num_tests=64, batch=32)
+    assert e.value.rc == _native.LDPC_EINVAL
+
+
 def test_random_regular_law():
     from iib_project_ldpc_codes_amd.graph import TannerGraph
     g = TannerGraph.random_regular(1000, 3, 6, seed=5)
