@@ -10,11 +10,17 @@ Weak scaling: every rank decodes its own 65536-frame batch.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Rank 0 prints one JSON line.  roofline: SURVEY.md 8(d) algorithmic bytes per
-codeword-iteration B_it = 2*E*4 + 2*n*4 = 320,000 B over the measured average
-kernel duration (HIP events on the launch stream).  cpu_baseline: the oracle's
-OpenMP fp32 sum-product (oracle/ldpc_oracle.c, "port": the reference has no
-soft decoder) on a bounded sample of the same frames.
+Rank 0 prints one JSON line.  roofline: the decode kernel keeps every edge
+message in LDS, so its binding unit is vector-instruction issue: VALU issue
+cycles per codeword-iteration (instruction mix of the committed HEAD profile,
+profiles/r02_valu_mix.json) x the live codeword-iteration rate of the kernel
+(HIP events on the launch stream) over 1024 SIMDs x 2.4 GHz.  roofline.hbm_model
+keeps SURVEY.md 8(d)'s streaming byte model (2*E*4 + 2*n*4 = 320,000 B per
+codeword-iteration, above the HBM peak by design) beside the measured HBM
+traffic (PMC FETCH_SIZE/WRITE_SIZE).  cpu_baseline: the oracle's OpenMP fp32
+sum-product ("port": the reference has no soft decoder) on all host cores this
+job may use and on one core, plus the reference's own message_passing.c (BEC
+hot path, configs[0] shape) on the same cores -- bounded samples, stated.
 """
 import argparse
 import json
@@ -60,65 +66,153 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=BATCH)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(graph, llr_host, seconds):
-    """Oracle fp32 SPA, OpenMP over frames, bounded to ~`seconds` of wall time."""
-    os.environ.setdefault("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1)))
-    from oracle import oracle
-    threads = oracle.num_threads()
-    csr = oracle.csr_from_lists(graph.variable_lookup, graph.check_lookup, graph.n, graph.m, DV, DC)
-    chunk = max(threads, 1) * 2
-    done = 0
+def host_cores():
+    """Host cores this process may use: the CPU affinity set, capped by a cgroup CPU quota
+    (the GPU box hands each one-GPU job a share of a larger machine; os.cpu_count() reports
+    the whole machine).  Returns (cores, os_cpu_count, detail)."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = total
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    cores = min(aff, quota) if quota else aff
+    return cores, total, {"os_cpu_count": total, "affinity": aff, "cgroup_quota_cpus": quota}
+
+
+def _timed(fn, chunk, seconds):
+    """Call fn(i) on successive chunks until `seconds` of wall time; returns (items, elapsed)."""
+    done, i = 0, 0
     t0 = time.perf_counter()
     while True:
-        sl = llr_host[done % llr_host.shape[0]:done % llr_host.shape[0] + chunk]
-        if sl.shape[0] < chunk:
-            sl = llr_host[:chunk]
-        oracle.bp_decode_batch(csr, sl, ITERS, 0)
-        done += sl.shape[0]
+        done += fn(i)
+        i += 1
         el = time.perf_counter() - t0
         if el >= seconds:
-            break
-    return {"value": done / el, "unit": "codewords/s", "cores": threads, "kind": "port",
-            "sample": f"{done} frames of the bench workload ((3,6) n=10000 BI-AWGN sigma={SIGMA}, "
-                      f"fp32 sum-product, 50 iterations) in {el:.1f} s, oracle/ldpc_oracle.c OpenMP "
-                      f"x{threads} threads (reference has no soft decoder)"}
+            return done, el
+
+
+def cpu_baseline(graph, llr_host, seconds):
+    """CPU baselines timed on this host in the same run (rank 0, N=1), on bounded samples.
+
+    value: the oracle's fp32 sum-product (oracle/ldpc_oracle.c, "port": the reference has no soft
+    decoder) on every host core this job may use, ~seconds*2/3; single_core: the same on one
+    thread; bec_reference_path: the reference's own message_passing.c (compiled unchanged into
+    oracle/_ref/ref_bench.so, one word per call as parallel_simulator.py:131-166) at the
+    configs[0] shape, all cores and one core."""
+    from oracle import oracle
+    cores, total, detail = host_cores()
+    csr = oracle.csr_from_lists(graph.variable_lookup, graph.check_lookup, graph.n, graph.m, DV, DC)
+    F = llr_host.shape[0]
+
+    def spa(threads, secs):
+        oracle.set_num_threads(threads)
+        chunk = 2 * threads
+
+        def fn(i):
+            lo = (i * chunk) % F
+            sl = llr_host[lo:lo + chunk] if lo + chunk <= F else llr_host[:chunk]
+            oracle.bp_decode_batch(csr, sl, ITERS, 0)
+            return sl.shape[0]
+        return _timed(fn, chunk, secs)
+
+    done_all, el_all = spa(cores, seconds * 0.45)
+    done_one, el_one = spa(1, seconds * 0.2)
+    out = {"value": done_all / el_all, "unit": "codewords/s", "cores": cores, "kind": "port",
+           "sample": f"{done_all} frames of the bench workload ((3,6) n=10000 BI-AWGN sigma={SIGMA}, fp32 "
+                     f"sum-product, 50 iterations; drawn from the first {F} frames of the batch) in "
+                     f"{el_all:.1f} s, oracle/ldpc_oracle.c OpenMP x{cores} threads (the reference has no "
+                     f"soft decoder)",
+           "host": detail,
+           "single_core": {"value": done_one / el_one, "unit": "codewords/s", "cores": 1,
+                           "sample": f"{done_one} frames in {el_one:.1f} s"}}
+    # the reference hot path itself: message_passing.c at configs[0] (n=1000, eps=0.4, 50 iterations)
+    gb = graph_cfg0()
+    words = oracle.channel(oracle.CH_BEC, 0.40, 5, 0, gb.n, 4096)
+    kind = "reference" if oracle.ref_bench_available() else "port"
+
+    def bec(threads, secs):
+        chunk = 64 * threads
+
+        def fn(i):
+            lo = (i * chunk) % words.shape[0]
+            sl = words[lo:lo + chunk] if lo + chunk <= words.shape[0] else words[:chunk]
+            if kind == "reference":
+                oracle.ref_bench_message_passing(sl, 50, gb.check_lookup, gb.variable_lookup, gb.n, gb.k,
+                                                 DV, DC, threads)
+            else:
+                oracle.set_num_threads(threads)
+                oracle.bec_decode_batch(sl, 50, gb.variable_lookup, gb.check_lookup, gb.n, gb.k, DV, DC)
+            return sl.shape[0]
+        return _timed(fn, chunk, secs)
+
+    b_all, e_all = bec(cores, seconds * 0.2)
+    b_one, e_one = bec(1, seconds * 0.15)
+    out["bec_reference_path"] = {
+        "value": b_all / e_all, "unit": "codewords/s", "cores": cores, "kind": kind,
+        "single_core": b_one / e_one,
+        "sample": f"configs[0] shape: (3,6) n=1000 BEC eps=0.4, 50 iterations; {b_all} words in {e_all:.1f} s "
+                  f"on {cores} threads, {b_one} in {e_one:.1f} s on one; "
+                  + ("reference message_passing.c compiled unchanged (oracle/_ref/ref_bench.so)"
+                     if kind == "reference" else "oracle restatement (reference build absent)")}
+    oracle.set_num_threads(cores)
+    return out
+
+
+def graph_cfg0():
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    return TannerGraph.random_regular(1000, DV, DC, seed=1)
+
+
+VALU_PROFILE = os.path.join(ROOT, "profiles", "r02_valu_mix.json")
+# issue cycles of one wave64 instruction on its SIMD at full rate (MI355X_MICROARCH.md, per-instruction
+# cycle constants: v_fma_f32 2 cycles on the SIMD-32; packed f32 twice that; transcendentals 8)
+VALU_CYCLES = {"packed": 4.0, "plain": 2.0, "trans": 8.0}
+SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 
 def valu_roofline(cw_iters_per_s):
-    """The unit that bounds the LDS kernel: vector-instruction issue.  VALU
-    wave-instructions per codeword-iteration come from the committed PMC profile of this kernel
-    (SQ_INSTS_VALU per launch / codeword-iterations); the live rate times that count is compared
-    with 256 CUs x 4 SIMDs issuing one wave64 VALU instruction per 4 cycles at 2.4 GHz
-    (transcendentals take 8, so frac understates the busy time: busy_frac_pmc is the profile's
-    SQ_ACTIVE_INST_VALU share at its own clock)."""
-    p = os.path.join(ROOT, "profiles", "r01f_pmc_summary.json")
-    if not os.path.exists(p):
+    """The binding unit of the LDS-resident kernel: vector-instruction issue.  Per codeword-
+    iteration wave-instruction counts by class (packed f32 / transcendental / other) come from the
+    committed HEAD profile (profiles/r02_valu_mix.json: SQ_INSTS_VALU and SQ_INSTS_VALU_TRANS_F32
+    per launch, the packed share from the kernel's ISA with each region's execution count);
+    achieved = issue cycles those instructions need x the live codeword-iteration rate; peak =
+    1024 SIMDs x 2.4 GHz."""
+    if not os.path.exists(VALU_PROFILE):
         return None
-    with open(p) as f:
+    with open(VALU_PROFILE) as f:
         d = json.load(f)
-    c, ns = d["counters"], d["dispatch_ns"]
-    per_it = c["SQ_INSTS_VALU"] / (BATCH * ITERS)
-    peak = 256 * 4 * 2.4e9 / 4
-    clock = c["GRBM_GUI_ACTIVE"] / 8 / (ns["GRBM_GUI_ACTIVE"] * 1e-9)
-    busy = c["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * ns["SQ_ACTIVE_INST_VALU"] * 1e-9 * clock)
-    achieved = per_it * cw_iters_per_s
-    return {"bound": "valu", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "G wave-instr/s",
-            "frac": achieved / peak, "valu_instr_per_codeword_iteration": per_it, "busy_frac_pmc": busy,
-            "note": "informational: the LDS-resident kernel is VALU-bound; instruction count from "
-                    "profiles/r01f_pmc_summary.json"}
+    per = d["wave_instr_per_codeword_iteration"]
+    cyc = sum(per[k] * VALU_CYCLES[k] for k in VALU_CYCLES)
+    achieved = cyc * cw_iters_per_s
+    peak = SIMDS * CLOCK_HZ
+    return {"bound": "valu", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "G SIMD-issue-cycles/s",
+            "frac": achieved / peak, "issue_cycles_per_codeword_iteration": cyc,
+            "wave_instr_per_codeword_iteration": per, "cycles_per_wave_instr": VALU_CYCLES,
+            "profile": os.path.relpath(VALU_PROFILE, ROOT), "profile_git": d.get("git")}
 
 
 def load_traffic():
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(p):
-        with open(p) as f:
-            return json.load(f)
+    for name in ("r02_pmc_traffic.json", "pmc_traffic.json"):
+        p = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(p):
+            with open(p) as f:
+                d = json.load(f)
+            d["source"] = "profiles/" + name
+            return d
     return None
 
 
@@ -267,7 +361,26 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(g, llr[:256].cpu().numpy(), args.cpu_seconds)
+        cpu = cpu_baseline(g, llr[:1024].cpu().numpy(), args.cpu_seconds)
+
+    hbm_model = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                 "frac": achieved / HBM_PEAK_GBPS, "algorithmic_bytes_per_codeword_iteration": b_it,
+                 "note": "SURVEY.md 8(d) streaming model (every edge message read + written through HBM "
+                         "each iteration); this kernel keeps the messages in LDS, so the model exceeds the "
+                         "HBM peak and is informational only"}
+    if traffic:
+        hbm_meas = traffic["bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9 * (B / traffic["batch"])
+        hbm_model["measured_traffic_bytes_per_launch"] = traffic["bytes_per_launch"] * B / traffic["batch"]
+        hbm_model["measured_GBps"] = hbm_meas
+        hbm_model["measured_frac"] = hbm_meas / HBM_PEAK_GBPS
+        hbm_model["measured_bytes_per_codeword"] = traffic["bytes_per_codeword"]
+        hbm_model["traffic_profile"] = traffic.get("source", "profiles/pmc_traffic.json")
+    roof = valu_roofline(kernel_cw_iters)
+    if roof is None:  # no instruction-mix profile: report the measured HBM use as the roofline
+        roof = {"bound": "hbm", "achieved": hbm_model.get("measured_GBps"), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": hbm_model.get("measured_frac")}
+    roof["traffic"] = hbm_model.get("measured_traffic_bytes_per_launch")
+    roof["hbm_model"] = hbm_model
 
     if rank == 0:
         line = {
@@ -292,17 +405,8 @@ def main():
             "codeword_iterations_per_s": value * ITERS,
             "kernel_ms_per_launch": kernel_ms,
             "fer_at_sigma": fer,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS,
-                         "traffic": traffic.get("bytes_per_launch") if traffic else None,
-                         "algorithmic_bytes_per_codeword_iteration": b_it,
-                         "note": "algorithmic bytes = SURVEY.md 8(d) streaming model; this kernel keeps the "
-                                 "messages in LDS, so its measured HBM traffic is "
-                                 + (f"{traffic['bytes_per_codeword'] / 1e3:.0f} KB" if traffic else "~100 KB")
-                                 + " per codeword (channel LLRs in, posteriors + decisions out), not "
-                                 f"{b_it * ITERS / 1e6:.0f} MB; the kernel is VALU-bound (DESIGN.md 3.1)"},
+            "roofline": roof,
             "lds_roofline": lds_roofline(g.n, g.m, DC, DV, kernel_cw_iters),
-            "valu_roofline": valu_roofline(kernel_cw_iters),
             "cpu_baseline": cpu,
             "extras": extras,
         }

@@ -60,6 +60,8 @@ def lib():
         _lib.oracle_check_update.restype = None
         _lib.oracle_num_threads.argtypes = []
         _lib.oracle_num_threads.restype = i
+        _lib.oracle_set_num_threads.argtypes = [i]
+        _lib.oracle_set_num_threads.restype = None
     return _lib
 
 
@@ -129,6 +131,10 @@ def check_update(x, algo=0, alpha=1.0):
 
 def num_threads():
     return int(lib().oracle_num_threads())
+
+
+def set_num_threads(t):
+    lib().oracle_set_num_threads(int(t))
 
 
 def philox(ctr, key):
@@ -283,3 +289,26 @@ def ref_generate_random_code(n, dv, dc):
             parity_check.ctypes.data_as(ct.POINTER(ct.c_bool)),
             ct.c_int(0), ct.c_bool(False), ct.c_int(0))
     return check_lookup, variable_lookup, parity_check.reshape(n - k, n)
+
+
+def ref_bench_available():
+    return os.path.exists(os.path.join(REF_DIR, "ref_bench.so"))
+
+
+def ref_bench_message_passing(words, iterations, check_lookup, variable_lookup, n, k, dv, dc, threads):
+    """The reference's own message_passing() (compiled unchanged into _ref/ref_bench.so) over a
+    batch of words, one call per word, OpenMP over words (oracle/ref_bench.c).
+    Returns (words_int32 [B, n], errors [B, iterations], its [B], threads_used)."""
+    lib_ = ct.CDLL(os.path.join(REF_DIR, "ref_bench.so"))
+    P, i = ct.c_void_p, ct.c_int
+    lib_.ref_bench_message_passing.argtypes = [P, i, i, P, P, P, P, i, i, i, i, i]
+    lib_.ref_bench_message_passing.restype = i
+    w = np.ascontiguousarray(words, dtype=np.int32).copy()
+    B = w.shape[0]
+    v2c = np.ascontiguousarray(variable_lookup, dtype=np.int32).ravel()
+    c2v = np.ascontiguousarray(check_lookup, dtype=np.int32).ravel()
+    err = np.zeros((B, iterations), np.int32)
+    its = np.zeros(B, np.int32)
+    used = lib_.ref_bench_message_passing(_p(w), B, iterations, _p(v2c), _p(c2v), _p(err), _p(its),
+                                          n, k, dv, dc, int(threads))
+    return w, err, its, used

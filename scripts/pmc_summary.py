@@ -15,11 +15,15 @@ d = sys.argv[1]
 batch = int(sys.argv[2]) if len(sys.argv) > 2 else None
 vals, dur, kern = {}, {}, {}
 for f in sorted(glob.glob(f"{d}/pmc*/run_counter_collection.csv")):
+    mine = {}
     for r in csv.DictReader(open(f)):
         k = r["Counter_Name"]
-        vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
+        if k in vals:  # the same counter in an earlier pass: keep that pass's value
+            continue
+        mine[k] = mine.get(k, 0.0) + float(r["Counter_Value"])
         dur[k] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         kern[k] = r["Kernel_Name"]
+    vals.update(mine)
 for k in sorted(vals):
     print(f"{k:28s} {vals[k]:20.1f}   dispatch_ns={dur[k]}")
 json.dump({"counters": vals, "dispatch_ns": dur, "kernel": kern}, open(f"{d}/pmc_summary.json", "w"), indent=1)
