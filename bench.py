@@ -90,7 +90,8 @@ def host_cores():
     except (OSError, ValueError):
         pass
     cores = min(aff, quota) if quota else aff
-    return cores, total, {"os_cpu_count": total, "affinity": aff, "cgroup_quota_cpus": quota}
+    env = {k: v for k, v in os.environ.items() if k.startswith(("OMP_", "GOMP_"))}
+    return cores, total, {"os_cpu_count": total, "affinity": aff, "cgroup_quota_cpus": quota, "omp_env": env}
 
 
 def _timed(fn, chunk, seconds):
@@ -144,6 +145,8 @@ def cpu_baseline(graph, llr_host, seconds):
     words = oracle.channel(oracle.CH_BEC, 0.40, 5, 0, gb.n, 4096)
     kind = "reference" if oracle.ref_bench_available() else "port"
 
+    used = []
+
     def bec(threads, secs):
         chunk = 64 * threads
 
@@ -151,8 +154,8 @@ def cpu_baseline(graph, llr_host, seconds):
             lo = (i * chunk) % words.shape[0]
             sl = words[lo:lo + chunk] if lo + chunk <= words.shape[0] else words[:chunk]
             if kind == "reference":
-                oracle.ref_bench_message_passing(sl, 50, gb.check_lookup, gb.variable_lookup, gb.n, gb.k,
-                                                 DV, DC, threads)
+                used.append(oracle.ref_bench_message_passing(sl, 50, gb.check_lookup, gb.variable_lookup, gb.n,
+                                                             gb.k, DV, DC, threads)[3])
             else:
                 oracle.set_num_threads(threads)
                 oracle.bec_decode_batch(sl, 50, gb.variable_lookup, gb.check_lookup, gb.n, gb.k, DV, DC)
@@ -163,7 +166,7 @@ def cpu_baseline(graph, llr_host, seconds):
     b_one, e_one = bec(1, seconds * 0.15)
     out["bec_reference_path"] = {
         "value": b_all / e_all, "unit": "codewords/s", "cores": cores, "kind": kind,
-        "single_core": b_one / e_one,
+        "single_core": b_one / e_one, "threads_reported_by_openmp": sorted(set(used)),
         "sample": f"configs[0] shape: (3,6) n=1000 BEC eps=0.4, 50 iterations; {b_all} words in {e_all:.1f} s "
                   f"on {cores} threads, {b_one} in {e_one:.1f} s on one; "
                   + ("reference message_passing.c compiled unchanged (oracle/_ref/ref_bench.so)"

@@ -20,9 +20,9 @@ int message_passing(int *Mvc, int iterations, int *variable_to_check_list, int *
 int ref_bench_message_passing(int *words, int B, int iterations, int *v2c, int *c2v, int *errors, int *its,
                               int n, int k, int dv, int dc, int threads)
 {
-    if (threads > 0) omp_set_num_threads(threads);
+    if (threads < 1) threads = 1;
     int used = 1;
-#pragma omp parallel
+#pragma omp parallel num_threads(threads)
     {
 #pragma omp single
         used = omp_get_num_threads();
