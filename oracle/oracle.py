@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+# ORACLE_LIB_PATH: the sanitizer build (scripts/sanitize.sh)
+LIB_PATH = os.environ.get("ORACLE_LIB_PATH") or os.path.join(HERE, "_build", "liboracle.so")
 REF_DIR = os.path.join(HERE, "_ref")
 
 _lib = None
