@@ -126,6 +126,22 @@ class MonteCarlo:
                 executor = device_executor(self)
         self.executor = executor
         self.rounds = 0
+        self.trial_base = 0   # first trial index of round 0 (a restored run continues here)
+        self.trial_base0 = 0  # first trial index of the whole run (snapshot trial range)
+
+    def next_trial(self):
+        """Index of the first trial the next round runs (all ranks)."""
+        return self.trial_base + self.rounds * self.world * self.batch
+
+    def snapshot(self, g=None):
+        """Counter snapshot of the run so far (collective when g is None; see snapshot.py)."""
+        from . import snapshot
+        return snapshot.from_counters(self, self._global() if g is None else g)
+
+    def restore(self, snap):
+        """Continue from a snapshot (snapshot.load(path)); see snapshot.restore."""
+        from . import snapshot
+        snapshot.restore(self, snap)
 
     @classmethod
     def ensemble(cls, n, dv, dc, channel, param, max_iters, **kw):
@@ -184,11 +200,13 @@ class MonteCarlo:
             return self.batch
         return int(max(0, min(self.batch, num_tests - trials_before - slot * self.batch)))
 
-    def run(self, num_tests, stop_frame_errors=200, time_limit=None):
+    def run(self, num_tests, stop_frame_errors=200, time_limit=None, checkpoint=None, checkpoint_every=1):
         """Run rounds until the global counters reach stop_frame_errors frame errors or
         num_tests trials, or time_limit seconds pass (parallel_simulator.py:198).  Counts
         equal one sequential process's over the same trials; the time limit is decided
-        collectively (every rank leaves on the same round)."""
+        collectively (every rank leaves on the same round).  checkpoint: snapshot path rank 0
+        rewrites every checkpoint_every rounds and at the end (snapshot.py)."""
+        from . import snapshot
         t0 = time.time()
         g = self._global()
         nc = len(self.counters)
@@ -198,7 +216,7 @@ class MonteCarlo:
                 break
             if num_tests and trials >= num_tests:
                 break
-            first_cw = (self.rounds * self.world + self.rank) * self.batch
+            first_cw = self.trial_base + (self.rounds * self.world + self.rank) * self.batch
             B = self._batch_size(num_tests, trials, self.rank)
             if self.world == 1:
                 # one process: the exact sequential stop happens inside the batch
@@ -232,8 +250,12 @@ class MonteCarlo:
                 self.rounds += 1
                 g = g + red[:len(red) - (self.world + 1)]
             frames, trials = self._frames_trials(g[:nc], g[nc:])
+            if checkpoint and self.rank == 0 and self.rounds % max(1, checkpoint_every) == 0:
+                snapshot.save(self.snapshot(g), checkpoint)
             if expired:
                 break
+        if checkpoint and self.rank == 0:
+            snapshot.save(self.snapshot(g), checkpoint)
         return self.results(g)
 
     def results(self, g=None):

@@ -19,7 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from iib_project_ldpc_codes_amd import de, ensembles  # noqa: E402
+from iib_project_ldpc_codes_amd import de, ensembles, snapshot  # noqa: E402
 from iib_project_ldpc_codes_amd.graph import TannerGraph  # noqa: E402
 from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo  # noqa: E402
 
@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--points", type=str, default=None)
+    ap.add_argument("--checkpoint-dir", type=str, default=None,
+                    help="snapshot each point there every round; a rerun resumes from it (snapshot.py)")
+    ap.add_argument("--seed", type=int, default=11)
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -50,10 +53,17 @@ def main():
         batch = args.batch or 16384
     rate = 1.0 - g.m / g.n
     for p in points:
-        mc = MonteCarlo(g, channel, p, iters, algo=algo, alpha=alpha, early_stop=True, seed=11, batch=batch)
+        mc = MonteCarlo(g, channel, p, iters, algo=algo, alpha=alpha, early_stop=True, seed=args.seed, batch=batch)
+        ck = None
+        if args.checkpoint_dir:
+            os.makedirs(args.checkpoint_dir, exist_ok=True)
+            ck = os.path.join(args.checkpoint_dir, f"{args.config}_p={p}_seed={args.seed}_B={batch}.json")
+            if os.path.exists(ck):
+                mc.restore(snapshot.load(ck))
         torch.cuda.synchronize()
         t0 = time.time()
-        res = mc.run(num_tests=args.trials, stop_frame_errors=200, time_limit=args.seconds)
+        trials0 = int(mc.snapshot()["counters"][0])
+        res = mc.run(num_tests=args.trials, stop_frame_errors=200, time_limit=args.seconds, checkpoint=ck)
         torch.cuda.synchronize()
         el = time.time() - t0
         if rank == 0:
@@ -61,7 +71,7 @@ def main():
                    "n": g.n, "rate": rate, "gpus": world, "trials": res["num_tests"],
                    "frame_errors": res["frame_errors"], "fer": res["fer"], "ber": res["ber"],
                    "mean_iterations": res["iterations"] / max(res["num_tests"], 1),
-                   "seconds": el, "codewords_per_s": res["num_tests"] / el}
+                   "seconds": el, "codewords_per_s": (res["num_tests"] - trials0) / el}
             if channel == "awgn":
                 out["ebn0_db"] = float(de.sigma_to_ebn0_db(p, rate))
             print(json.dumps(out), flush=True)
