@@ -109,9 +109,9 @@ def _timed(fn, chunk, seconds):
 def cpu_baseline(graph, llr_host, seconds):
     """CPU baselines timed on this host in the same run (rank 0, N=1), on bounded samples.
 
-    value: the oracle's fp32 sum-product (oracle/ldpc_oracle.c, "port": the reference has no soft
-    decoder) on every host core this job may use, ~seconds*2/3; single_core: the same on one
-    thread; bec_reference_path: the reference's own message_passing.c (compiled unchanged into
+    value: the oracle's fp32 sum-product in the GPU kernel's formulation (oracle/ldpc_oracle.c
+    algo 2, "port": the reference has no soft decoder) on every host core this job may use;
+    single_core: the same on one thread; bec_reference_path: the reference's own message_passing.c (compiled unchanged into
     oracle/_ref/ref_bench.so, one word per call as parallel_simulator.py:131-166) at the
     configs[0] shape, all cores and one core."""
     from oracle import oracle
@@ -126,7 +126,7 @@ def cpu_baseline(graph, llr_host, seconds):
         def fn(i):
             lo = (i * chunk) % F
             sl = llr_host[lo:lo + chunk] if lo + chunk <= F else llr_host[:chunk]
-            oracle.bp_decode_batch(csr, sl, ITERS, 0)
+            oracle.bp_decode_batch(csr, sl, ITERS, 2)  # algo 2: fp32, the GPU kernel's check formulation
             return sl.shape[0]
         return _timed(fn, chunk, secs)
 
@@ -135,8 +135,8 @@ def cpu_baseline(graph, llr_host, seconds):
     out = {"value": done_all / el_all, "unit": "codewords/s", "cores": cores, "kind": "port",
            "sample": f"{done_all} frames of the bench workload ((3,6) n=10000 BI-AWGN sigma={SIGMA}, fp32 "
                      f"sum-product, 50 iterations; drawn from the first {F} frames of the batch) in "
-                     f"{el_all:.1f} s, oracle/ldpc_oracle.c OpenMP x{cores} threads (the reference has no "
-                     f"soft decoder)",
+                     f"{el_all:.1f} s, oracle/ldpc_oracle.c algo 2 (fp32, the kernel's elementary-symmetric check "
+                     f"form) OpenMP x{cores} threads (the reference has no soft decoder)",
            "host": detail,
            "single_core": {"value": done_one / el_one, "unit": "codewords/s", "cores": 1,
                            "sample": f"{done_one} frames in {el_one:.1f} s"}}

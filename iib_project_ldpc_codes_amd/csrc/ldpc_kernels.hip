@@ -46,6 +46,12 @@ constexpr int kWave = 64;
 #ifndef LDPC_ABLATE_CHECK
 #define LDPC_ABLATE_CHECK 0
 #endif
+#ifndef LDPC_SPA_RWIRE
+#define LDPC_SPA_RWIRE 1  // bp_lds_kernel sum-product: v->c wire = the clamped ratio R itself (see ratio_wire)
+#endif
+#ifndef LDPC_ABLATE_VARIO
+#define LDPC_ABLATE_VARIO 0  // timing ablation only: 1 = no variable-phase stores, 2 = no gathers
+#endif
 #ifndef LDPC_ABLATE_BARRIER
 #define LDPC_ABLATE_BARRIER 0  // timing ablation only: 1 = drop the two per-iteration barriers (racy)
 #endif
@@ -699,11 +705,21 @@ __device__ __forceinline__ float2 v2c_wire2(float2 x) {
 // v_rcp_f32 in place of the v_exp_f32, one packed subtraction per two edges.
 // (The algebraically equal (Rc - 1) / max(Rc, 1) forms 1 - a ~ 1/R as a difference
 // of two numbers near 1 and loses it to rounding for large R.)
+//
+// LDPC_SPA_RWIRE: the wire carries R itself, clamped to [2^-23, 2^23] (|x| <= 23, as
+// above), and the check forms the pair (R - 1, R + 1) = (a, b) * (R + 1) / 2 instead of
+// (a, 2 - |a|): tanh(x/2) = (R - 1) / (R + 1), and the check rule's outputs
+// (D + N) / (D - N) are invariant to a positive scale of each input's (a, b).  No
+// reciprocal per edge in the variable phase; magnitudes stay below 2^23 + 1, so the
+// exclusive products of 5 inputs stay below 2^116.
 __device__ __forceinline__ float ratio_wire(float R) {
+    if (LDPC_SPA_RWIRE) return __builtin_amdgcn_fmed3f(R, 0x1p-23f, 0x1p23f);
     return __builtin_amdgcn_fmed3f(R, 0x1p-23f, 1.0f) -
            __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(R), 0x1p-23f, 1.0f);
 }
 __device__ __forceinline__ float2 ratio_wire2(float2 R) {
+    if (LDPC_SPA_RWIRE)
+        return make_float2(__builtin_amdgcn_fmed3f(R.x, 0x1p-23f, 0x1p23f), __builtin_amdgcn_fmed3f(R.y, 0x1p-23f, 0x1p23f));
     const float2 lo = make_float2(__builtin_amdgcn_fmed3f(R.x, 0x1p-23f, 1.0f),
                                   __builtin_amdgcn_fmed3f(R.y, 0x1p-23f, 1.0f));
     const float2 u = make_float2(__builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(R.x), 0x1p-23f, 1.0f),
@@ -768,7 +784,7 @@ __device__ __forceinline__ void check_update(float (&x)[D], float alpha, int d =
 // packed op for both checks.  a[] holds the wire values in and the outputs out.
 // 2 - |x| as one VOP3 op with an abs modifier (the vectoriser would otherwise
 // pack it as v_and + v_pk_add, 1.5 ops per value)
-__device__ __forceinline__ float two_minus_abs(float x) {
+[[maybe_unused]] __device__ __forceinline__ float two_minus_abs(float x) {
     float r;
     asm("v_sub_f32_e64 %0, 2.0, |%1|" : "=v"(r) : "v"(x));
     return r;
@@ -847,6 +863,48 @@ __device__ __forceinline__ void check_update_spa_pair(float2 (&a)[D]) {
         a[i] = r;
     }
     a[0] = out(sn, one, sd);
+}
+
+// LDPC_SPA_RWIRE form of check_update_spa_pair<D, false>: the inputs are the clamped
+// ratios R_i = e^{x_i} (ratio_wire), and tanh(x_i/2) = (R_i - 1) / (R_i + 1).  With
+// D_j = prod_{i != j} (R_i + 1) and N_j = prod_{i != j} (R_i - 1), the output ratio
+// (D_j + N_j) / (D_j - N_j) is, expanding both products in the elementary symmetric
+// polynomials e_k of the d - 1 inputs i != j, O_j / E_j for d - 1 odd (E_j / O_j for
+// d - 1 even), where E = sum_{k even} e_k and O = sum_{k odd} e_k.  Every term is
+// positive, so there is no cancellation anywhere (the difference D - N of the ratio
+// form loses ~d ulps x e^|c| near saturation): each output is good to ~10 fp32 ulps.
+// (E, O) of a set grows by one input R as (E + R O, O + R E) -- two fused multiply-adds,
+// the cost of the ratio form's two product chains -- and two disjoint sets combine as
+// (E_a E_b + O_a O_b, E_a O_b + O_a E_b).  Magnitudes: E >= 1, O >= sum R >= 2^-23,
+// e_k < 2^(23 k + 3) <= 2^118 for the 5 inputs of a degree-6 check.
+template <int D>
+__device__ __forceinline__ void check_update_spa_pair_rwire(float2 (&R)[D]) {
+    const float2 one = make_float2(1.0f, 1.0f);
+    auto ratio = [](float2 E, float2 O) {
+        if constexpr ((D - 1) % 2 == 1) return O * make_float2(__builtin_amdgcn_rcpf(E.x), __builtin_amdgcn_rcpf(E.y));
+        else return E * make_float2(__builtin_amdgcn_rcpf(O.x), __builtin_amdgcn_rcpf(O.y));
+    };
+    float2 pE[D], pO[D];  // prefix sets {0 .. i-1}
+    pE[1] = one;
+    pO[1] = R[0];
+#pragma unroll
+    for (int i = 2; i < D; ++i) {
+        pE[i] = pk_fma(R[i - 1], pO[i - 1], pE[i - 1]);
+        pO[i] = pk_fma(R[i - 1], pE[i - 1], pO[i - 1]);
+    }
+    float2 sE = one, sO = R[D - 1];  // suffix set {i+1 .. D-1}
+    R[D - 1] = ratio(pE[D - 1], pO[D - 1]);
+#pragma unroll
+    for (int i = D - 2; i >= 1; --i) {
+        const float2 E = pk_fma(pE[i], sE, pO[i] * sO);
+        const float2 O = pk_fma(pE[i], sO, pO[i] * sE);
+        const float2 nE = pk_fma(R[i], sO, sE);
+        const float2 nO = pk_fma(R[i], sE, sO);
+        R[i] = ratio(E, O);
+        sE = nE;
+        sO = nO;
+    }
+    R[0] = ratio(sE, sO);
 }
 
 // Byte address (x4) of the low / high 16-bit LDS position packed in p: one SDWA
@@ -989,7 +1047,9 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
         __syncthreads();  // staging read before the message initialisation overwrites it
 #pragma unroll
         for (int i = 0; i < VPT; ++i) {
-            const float w = v2c_wire<ALGO>(L[i]);
+            const float w = LDPC_SPA_RWIRE && ALGO == 0 && LDPC_SPA_PROD
+                                ? __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[i], -23.0f, 23.0f))
+                                : v2c_wire<ALGO>(L[i]);
 #pragma unroll
             for (int j = 0; j < DV; ++j) at(addr(i, j)) = w;
         }
@@ -1067,7 +1127,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     a1[j] = addr(i + 1, j);
                 }
 #pragma unroll
-                for (int j = 0; j < DV; ++j) cv[j] = make_float2(at(a0[j]), at(a1[j]));
+                for (int j = 0; j < DV; ++j) if (LDPC_ABLATE_VARIO != 2) cv[j] = make_float2(at(a0[j]), at(a1[j]));
                 if constexpr (FINAL) {
                     float2 s = make_float2(llr_log2(i), llr_log2(i + 1));
 #pragma unroll
@@ -1075,10 +1135,21 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                         s = s + make_float2(__builtin_amdgcn_logf(cv[j].x), __builtin_amdgcn_logf(cv[j].y));
                     if constexpr (!MC) { pr[i] = s.x; pr[i + 1] = s.y; }
                 } else {
+                    if constexpr (LDPC_ABLATE_VARIO == 2) {
+#pragma unroll
+                        for (int j = 0; j < DV; ++j) {
+                            cv[j] = make_float2(__uint_as_float(a0[j]) , __uint_as_float(a1[j]));
+                            asm volatile("" : "+v"(cv[j].x), "+v"(cv[j].y));
+                        }
+                    }
                     const float2 post = edges(cv, make_float2(L[i], L[i + 1]), [&](int j, float2 R) {
                         const float2 w = ratio_wire2(R);
-                        at(a0[j]) = w.x;
-                        at(a1[j]) = w.y;
+                        if constexpr (LDPC_ABLATE_VARIO == 1) {
+                            asm volatile("" :: "v"(w.x), "v"(w.y));
+                        } else {
+                            at(a0[j]) = w.x;
+                            at(a1[j]) = w.y;
+                        }
                     });
                     if constexpr (ET) {
                         put_hard(i, post.x < 1.0f, a0);
@@ -1220,7 +1291,8 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                 for (int i = 0; i < DC; ++i) x2[i] = x2[i] * make_float2(0.5f, 0.5f);  // timing ablation only
 #else
                 if constexpr (ALGO == 0) {
-                    check_update_spa_pair<DC, !PROD>(x2);
+                    if constexpr (LDPC_SPA_RWIRE && PROD) check_update_spa_pair_rwire<DC>(x2);
+                    else check_update_spa_pair<DC, !PROD>(x2);
                 } else {
                     float xa[DC], xb[DC];
 #pragma unroll
