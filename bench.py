@@ -11,10 +11,11 @@ Weak scaling: every rank decodes its own 65536-frame batch.
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Rank 0 prints one JSON line.  roofline: the decode kernel keeps every edge
-message in LDS, so its binding unit is vector-instruction issue: VALU issue
-cycles per codeword-iteration (instruction mix of the committed HEAD profile,
-profiles/r02_valu_mix.json) x the live codeword-iteration rate of the kernel
-(HIP events on the launch stream) over 1024 SIMDs x 2.4 GHz.  roofline.hbm_model
+message in LDS, so its binding unit is on-chip: LDS cycles (per CU) or VALU
+issue cycles (per SIMD) per codeword-iteration from the committed HEAD issue
+model (profiles/r02b_issue_model.json, scripts/issue_model.py) x the live
+codeword-iteration rate of the kernel (HIP events on the launch stream) over
+the unit's peak; the larger fraction is `roofline`.  roofline.hbm_model
 keeps SURVEY.md 8(d)'s streaming byte model (2*E*4 + 2*n*4 = 320,000 B per
 codeword-iteration, above the HBM peak by design) beside the measured HBM
 traffic (PMC FETCH_SIZE/WRITE_SIZE).  cpu_baseline: the oracle's OpenMP fp32
@@ -36,30 +37,6 @@ ITERS = 50
 BATCH = 65536
 SIGMA = 0.85
 HBM_PEAK_GBPS = 8000.0
-# LDS rates per CU per clock by instruction (MI355X_MICROARCH.md, LDS table), 256 CUs at ~2.4 GHz
-LDS_CHIP = 256 * 2.4e9
-LDS_B_PER_CLK = {"ds_read_b128": 256.0, "ds_read_b32": 128.0, "ds_write_b128": 79.0, "ds_write_b32": 64.0}
-
-
-def lds_roofline(n, m, dc, dv, cw_iters_per_s):
-    """The LDS-resident kernel's own bound: every iteration reads and writes each edge message
-    once in the check phase (check pairs, contiguous ds_read_b128 / ds_write_b128) and once in the
-    variable phase (gathered, ds_read_b32 / ds_write_b32).  Peak = those bytes at the
-    instruction rates."""
-    chk = m * dc * 4
-    var = n * dv * 4
-    t_peak = (chk / LDS_B_PER_CLK["ds_read_b128"] + chk / LDS_B_PER_CLK["ds_write_b128"]
-              + var / LDS_B_PER_CLK["ds_read_b32"] + var / LDS_B_PER_CLK["ds_write_b32"]) / LDS_CHIP
-    bytes_it = 2 * (chk + var)
-    peak = bytes_it / t_peak / 1e9
-    achieved = bytes_it * cw_iters_per_s / 1e9
-    return {"bound": "lds", "achieved": achieved, "peak": peak, "unit": "GB/s", "frac": achieved / peak,
-            "bytes_per_codeword_iteration": bytes_it,
-            "note": "informational: the unit this kernel is closest to (messages live in LDS); peak = the "
-                    "per-instruction LDS rates of MI355X_MICROARCH.md for this access mix; the kernel "
-                    "itself is VALU-bound (DESIGN.md 3.1)"}
-
-
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -180,32 +157,38 @@ def graph_cfg0():
     return TannerGraph.random_regular(1000, DV, DC, seed=1)
 
 
-VALU_PROFILE = os.path.join(ROOT, "profiles", "r02_valu_mix.json")
-# issue cycles of one wave64 instruction on its SIMD at full rate (MI355X_MICROARCH.md, per-instruction
-# cycle constants: v_fma_f32 2 cycles on the SIMD-32; packed f32 twice that; transcendentals 8)
-VALU_CYCLES = {"packed": 4.0, "plain": 2.0, "trans": 8.0}
-SIMDS, CLOCK_HZ = 1024, 2.4e9
+ISSUE_PROFILE = os.path.join(ROOT, "profiles", "r02b_issue_model.json")
+SIMDS, CUS, CLOCK_HZ = 1024, 256, 2.4e9
 
 
-def valu_roofline(cw_iters_per_s):
-    """The binding unit of the LDS-resident kernel: vector-instruction issue.  Per codeword-
-    iteration wave-instruction counts by class (packed f32 / transcendental / other) come from the
-    committed HEAD profile (profiles/r02_valu_mix.json: SQ_INSTS_VALU and SQ_INSTS_VALU_TRANS_F32
-    per launch, the packed share from the kernel's ISA with each region's execution count);
-    achieved = issue cycles those instructions need x the live codeword-iteration rate; peak =
-    1024 SIMDs x 2.4 GHz."""
-    if not os.path.exists(VALU_PROFILE):
-        return None
-    with open(VALU_PROFILE) as f:
+def onchip_rooflines(cw_iters_per_s):
+    """The units the LDS-resident kernel can saturate, from the committed HEAD issue model
+    (profiles/r02b_issue_model.json, scripts/issue_model.py: the kernel ISA's blocks x their
+    execution counts, cross-checked with and completed by the PMC counters of one launch):
+      valu: issue cycles per codeword-iteration (packed f32 4, plain 2, transcendental 8 per
+            wave64 instruction, MI355X_MICROARCH.md) over 1024 SIMDs x 2.4 GHz;
+      lds:  LDS cycles per codeword-iteration (per-instruction costs of the MI355X_MICROARCH.md
+            LDS table + measured bank-conflict cycles) over 256 CUs x 2.4 GHz.
+    achieved = cycles x the live codeword-iteration rate of the kernel.  Returns (valu, lds)."""
+    if not os.path.exists(ISSUE_PROFILE):
+        return None, None
+    with open(ISSUE_PROFILE) as f:
         d = json.load(f)
-    per = d["wave_instr_per_codeword_iteration"]
-    cyc = sum(per[k] * VALU_CYCLES[k] for k in VALU_CYCLES)
-    achieved = cyc * cw_iters_per_s
-    peak = SIMDS * CLOCK_HZ
-    return {"bound": "valu", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "G SIMD-issue-cycles/s",
-            "frac": achieved / peak, "issue_cycles_per_codeword_iteration": cyc,
-            "wave_instr_per_codeword_iteration": per, "cycles_per_wave_instr": VALU_CYCLES,
-            "profile": os.path.relpath(VALU_PROFILE, ROOT), "profile_git": d.get("git")}
+    rel = os.path.relpath(ISSUE_PROFILE, ROOT)
+    v_cyc = d["valu_issue_cycles_per_codeword_iteration"]
+    l_cyc = d["lds_cycles_per_codeword_iteration"]
+    valu = {"bound": "valu", "achieved": v_cyc * cw_iters_per_s / 1e9, "peak": SIMDS * CLOCK_HZ / 1e9,
+            "unit": "G SIMD-issue-cycles/s", "frac": v_cyc * cw_iters_per_s / (SIMDS * CLOCK_HZ),
+            "issue_cycles_per_codeword_iteration": v_cyc,
+            "wave_instr_per_codeword_iteration": d["wave_instr_per_codeword_iteration"],
+            "cycles_per_wave_instr": d["cycles"]["valu"], "profile": rel, "profile_git": d.get("git")}
+    lds = {"bound": "lds", "achieved": l_cyc * cw_iters_per_s / 1e9, "peak": CUS * CLOCK_HZ / 1e9,
+           "unit": "G LDS-cycles/s", "frac": l_cyc * cw_iters_per_s / (CUS * CLOCK_HZ),
+           "lds_cycles_per_codeword_iteration": l_cyc,
+           "lds_instr_per_codeword_iteration": d["lds_instr_per_codeword_iteration"],
+           "bank_conflict_cycles_per_codeword_iteration": d["lds_bank_conflict_cycles_per_codeword_iteration"],
+           "cycles_per_wave_instr": d["cycles"]["lds"], "profile": rel, "profile_git": d.get("git")}
+    return valu, lds
 
 
 def load_traffic():
@@ -378,10 +361,14 @@ def main():
         hbm_model["measured_frac"] = hbm_meas / HBM_PEAK_GBPS
         hbm_model["measured_bytes_per_codeword"] = traffic["bytes_per_codeword"]
         hbm_model["traffic_profile"] = traffic.get("source", "profiles/pmc_traffic.json")
-    roof = valu_roofline(kernel_cw_iters)
-    if roof is None:  # no instruction-mix profile: report the measured HBM use as the roofline
+    valu_roof, lds_roof = onchip_rooflines(kernel_cw_iters)
+    if lds_roof is None:  # no issue-model profile: report the measured HBM use as the roofline
         roof = {"bound": "hbm", "achieved": hbm_model.get("measured_GBps"), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": hbm_model.get("measured_frac")}
+    else:  # the binding unit is the one with the larger fraction
+        roof = dict(max((lds_roof, valu_roof), key=lambda r: r["frac"]))
+        roof["other_units"] = {r["bound"]: {"frac": r["frac"], "achieved": r["achieved"], "peak": r["peak"],
+                                            "unit": r["unit"]} for r in (lds_roof, valu_roof) if r is not roof}
     roof["traffic"] = hbm_model.get("measured_traffic_bytes_per_launch")
     roof["hbm_model"] = hbm_model
 
@@ -409,7 +396,8 @@ def main():
             "kernel_ms_per_launch": kernel_ms,
             "fer_at_sigma": fer,
             "roofline": roof,
-            "lds_roofline": lds_roofline(g.n, g.m, DC, DV, kernel_cw_iters),
+            "valu_roofline": valu_roof,
+            "lds_roofline": lds_roof,
             "cpu_baseline": cpu,
             "extras": extras,
         }

@@ -23,7 +23,7 @@ constexpr int kWave = 64;
 #define LDPC_VAR_PAIRS 1  // variable pairs per sched_barrier group in the LDS kernel's variable phase
 #endif
 #ifndef LDPC_CHECK_PAIRS_UNROLL
-#define LDPC_CHECK_PAIRS_UNROLL 1  // check pairs per iteration of the LDS kernel's check loop
+#define LDPC_CHECK_PAIRS_UNROLL 2  // check pairs per iteration of the LDS kernel's check loop (1: 1.4 % slower)
 #endif
 #ifndef LDPC_BEC_BITS
 #define LDPC_BEC_BITS 1  // fixed-code BEC Monte-Carlo on the bit-sliced kernel when its planes fit LDS
@@ -48,6 +48,9 @@ constexpr int kWave = 64;
 #endif
 #ifndef LDPC_SPA_RWIRE
 #define LDPC_SPA_RWIRE 1  // bp_lds_kernel sum-product: v->c wire = the clamped ratio R itself (see ratio_wire)
+#endif
+#ifndef LDPC_CHECK_W64
+#define LDPC_CHECK_W64 0  // check phase writes each pair edge with its own ds_write_b64
 #endif
 #ifndef LDPC_ABLATE_VARIO
 #define LDPC_ABLATE_VARIO 0  // timing ablation only: 1 = no variable-phase stores, 2 = no gathers
@@ -1309,7 +1312,18 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                 }
 #endif
 #pragma unroll
-                for (int i = 0; i < DC; ++i) pp[i] = x2[i];
+                for (int i = 0; i < DC; ++i) {
+                    if constexpr (LDPC_CHECK_W64) {
+                        // one ds_write_b64 per edge of the pair: 3 source dwords = 6 cycles per
+                        // 8 bytes, where ds_write_b128 moves 16 bytes in ~13 (MI355X_MICROARCH.md)
+                        const f32x2 v = {x2[i].x, x2[i].y};
+                        asm volatile("ds_write_b64 %0, %1 offset:%2"
+                                     :: "v"((uint32_t)(size_t)(lds_u8 *)(pp + i) - 8u * i), "v"(v), "i"(8 * i)
+                                     : "memory");
+                    } else {
+                        pp[i] = x2[i];
+                    }
+                }
             }
             if constexpr (ET) {
                 if (!__syncthreads_or(unsat | (it == 0))) break;
