@@ -167,8 +167,9 @@ def onchip_rooflines(cw_iters_per_s):
     execution counts, cross-checked with and completed by the PMC counters of one launch):
       valu: issue cycles per codeword-iteration (packed f32 4, plain 2, transcendental 8 per
             wave64 instruction, MI355X_MICROARCH.md) over 1024 SIMDs x 2.4 GHz;
-      lds:  LDS cycles per codeword-iteration (per-instruction costs of the MI355X_MICROARCH.md
-            LDS table + measured bank-conflict cycles) over 256 CUs x 2.4 GHz.
+      lds:  LDS cycles per codeword-iteration (conflict-free per-instruction costs of the
+            MI355X_MICROARCH.md LDS table; the measured bank-conflict cycles are reported
+            beside it as waste) over 256 CUs x 2.4 GHz.
     achieved = cycles x the live codeword-iteration rate of the kernel.  Returns (valu, lds)."""
     if not os.path.exists(ISSUE_PROFILE):
         return None, None
@@ -192,7 +193,7 @@ def onchip_rooflines(cw_iters_per_s):
 
 
 def load_traffic():
-    for name in ("r02_pmc_traffic.json", "pmc_traffic.json"):
+    for name in ("r02b_pmc_traffic.json", "r02_pmc_traffic.json", "pmc_traffic.json"):
         p = os.path.join(ROOT, "profiles", name)
         if os.path.exists(p):
             with open(p) as f:
