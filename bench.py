@@ -321,7 +321,7 @@ def main():
         # configs[3] shape: irregular RSU rate-1/2 ensemble (density-evolution lambda/rho),
         # n = 20000, BI-AWGN sum-product, 100 iterations, fixed count and with early stop
         from iib_project_ldpc_codes_amd import ensembles
-        gi = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1)
+        gi = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1, deg2="zigzag")
         Bi = 8192
         llr_i = decoder.channel_dev("awgn", 0.80, 7, 0, gi.n, Bi)
         for key, et in (("irregular_cfg4_n20000_spa_100it", False), ("irregular_cfg4_n20000_spa_early_stop", True)):

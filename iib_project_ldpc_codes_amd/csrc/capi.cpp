@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <map>
@@ -19,6 +20,9 @@
 
 #ifndef LDPC_IRR
 #define LDPC_IRR 1  // irregular graphs on bp_irr_kernel when in range
+#endif
+#ifndef LDPC_LOC_LAYOUT
+#define LDPC_LOC_LAYOUT 1  // build the local-edge layout (bp_loc_kernel) for rate-1/2 graphs
 #endif
 #include "ldpc_mi355x.h"
 
@@ -399,6 +403,37 @@ int device_graph(const HostGraph &h, ldpc_graph **out) {
         g->lane_T = T;
         g->lane_VPT = VPT;
     }
+    // LDPC_NO_LOC_LAYOUT=1 in the environment: no local-edge layout (tests run the
+    // other kernels on the same graphs)
+    const char *noloc = getenv("LDPC_NO_LOC_LAYOUT");
+    if (e == hipSuccess && h.consistent && LDPC_LOC_LAYOUT && !(noloc && noloc[0] == '1')) {
+        LocLayout L;
+        // threads: 256 for up to 1024 check pairs (4 per thread), 1024 for up to 3072 (3 per
+        // thread: 4 do not fit 128 VGPRs), else 512 threads with 256 VGPRs (up to 10 per thread)
+        const int P = h.m / 2;
+        L.T = P <= 1024 ? 256 : (P <= 3072 ? 1024 : 512);
+        if (build_loc_layout(h.n, h.m, h.cptr, h.cvar, h.vptr, h.vslot, L)) {
+            e = upload(&g->loc_var, L.var);
+            if (e == hipSuccess) e = upload(&g->loc_pos, L.pos);
+            if (e == hipSuccess) e = upload(&g->loc_info, L.info);
+            g->loc_T = L.T; g->loc_KP = L.KP; g->loc_DVN = L.DVN; g->loc_P = L.P;
+            g->loc_ncls = L.ncls; g->loc_words = L.words;
+            int dlo = 99, dhi = 0;
+            bool mix_ok = true;
+            for (int i = 0; i < L.ncls; ++i) {
+                dlo = std::min(dlo, L.cls_d[i] >> 8 ? L.cls_d[i] >> 8 : L.cls_d[i]);
+                dhi = std::max(dhi, L.cls_d[i] & 255);
+            }
+            for (int i = 0; i < L.ncls; ++i)  // the kernel pads a mixed pair's smaller check by one input
+                if (L.cls_d[i] >> 8) mix_ok &= (L.cls_d[i] & 255) == dhi && (L.cls_d[i] >> 8) == dhi - 1;
+            g->loc_dlo = dlo; g->loc_dhi = dhi;
+            if (!mix_ok) g->loc_KP = 0;
+            for (int i = 0; i <= L.ncls; ++i) { g->loc_cls_q[i] = L.cls_q[i]; g->loc_cls_w[i] = L.cls_w[i]; }
+            for (int i = 0; i < L.ncls; ++i) g->loc_cls_d[i] = L.cls_d[i];
+            g->loc_dvn0 = L.DVN0; g->loc_dvn1 = L.DVN1;
+            g->loc_abs0 = L.ABS0; g->loc_abs1 = L.ABS1;
+        }
+    }
     if (e == hipSuccess && h.consistent && !g->lane_var && LDPC_IRR) {
         std::vector<int32_t> ln, cd;
         int VPT_ = 0, KC = 0, DC = 0, S = 0, P = 0;
@@ -486,6 +521,9 @@ void ldpc_graph_destroy(ldpc_graph *g) {
     (void)hipFree(g->lane_slot);
     (void)hipFree(g->irr_lane);
     (void)hipFree(g->irr_cdeg);
+    (void)hipFree(g->loc_var);
+    (void)hipFree(g->loc_pos);
+    (void)hipFree(g->loc_info);
     delete g;
 }
 
@@ -530,6 +568,37 @@ int ldpc_debug_irr_layout(const int32_t *check_ptr, const int32_t *check_var, co
     shape[0] = VPT; shape[1] = KC; shape[2] = DC; shape[3] = S; shape[4] = P;
     if (lane) std::copy(ln.begin(), ln.end(), lane);
     if (cdeg) std::copy(cd.begin(), cd.end(), cdeg);
+    return LDPC_OK;
+}
+
+int ldpc_debug_loc_layout(const int32_t *check_ptr, const int32_t *check_var, const int32_t *var_ptr,
+                          const int32_t *var_slot, int n, int m, int T, int32_t *shape, int32_t *var, int32_t *pos,
+                          int32_t *info) {
+    LDPC_REQUIRE(shape, "null shape");
+    LDPC_REQUIRE(T == 256 || T == 512 || T == 1024, "T must be 256, 512 or 1024");
+    HostGraph h;
+    int rc = host_graph_from_csr(check_ptr, check_var, var_ptr, var_slot, n, m, h);
+    if (rc) return rc;
+    LocLayout L;
+    L.T = T;
+    if (!h.consistent || !build_loc_layout(h.n, h.m, h.cptr, h.cvar, h.vptr, h.vslot, L)) {
+        set_error("graph has no local-edge layout (needs n = 2m, a perfect local matching, even degree classes)");
+        return LDPC_EUNSUP;
+    }
+    shape[0] = L.T; shape[1] = L.KP; shape[2] = L.DVN; shape[3] = L.P; shape[4] = L.words;
+    shape[5] = L.ncls; shape[6] = (int32_t)std::min<long>(L.conflicts, 0x7fffffff);
+    for (int i = 0; i < kLocMaxCls; ++i) {
+        shape[7 + i] = L.cls_q[i];
+        shape[7 + kLocMaxCls + 1 + i] = L.cls_d[i];
+        shape[7 + 2 * kLocMaxCls + 1 + i] = L.cls_w[i];
+    }
+    shape[7 + kLocMaxCls] = L.cls_q[kLocMaxCls];
+    shape[7 + 3 * kLocMaxCls + 1] = L.cls_w[kLocMaxCls];
+    shape[22] = L.DVN0 | (L.ABS0 ? 256 : 0);
+    shape[23] = L.DVN1 | (L.ABS1 ? 256 : 0);
+    if (var) std::copy(L.var.begin(), L.var.end(), var);
+    if (pos) std::copy(L.pos.begin(), L.pos.end(), pos);
+    if (info) std::copy(L.info.begin(), L.info.end(), info);
     return LDPC_OK;
 }
 

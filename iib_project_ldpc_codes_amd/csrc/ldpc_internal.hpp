@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 // Device-resident Tanner graph.  Slot e = position in the check-major edge
 // list (the reference's check_lookup order, random_code_generator.c:34-36).
@@ -37,7 +38,28 @@ struct ldpc_graph {
     int32_t *irr_lane = nullptr;  // [3][1024*VPT]: variable id (-1 pad), positions j0|j1<<16, j2|j3<<16
                                   // (0xFFFF = no edge; lanes of one 64-lane row share a degree)
     int32_t *irr_cdeg = nullptr;  // [2][1024]: degrees of thread t's checks, 4 bits per row k
+    // Local-edge layout of bp_loc_kernel (build_loc_layout, loc_layout.cpp); loc_KP == 0: none
+    int loc_T = 0, loc_KP = 0, loc_DVN = 0, loc_P = 0, loc_ncls = 0, loc_words = 0, loc_dlo = 0, loc_dhi = 0;
+    int loc_dvn0 = 0, loc_dvn1 = 0;       // non-local edges per variable, local slot 0 / 1 (max)
+    bool loc_abs0 = false, loc_abs1 = false;  // some variable of that slot has fewer
+    int loc_cls_q[5] = {0}, loc_cls_d[4] = {0}, loc_cls_w[5] = {0};
+    int32_t *loc_var = nullptr;   // [2*KP][2][T] variable id of var pair (thread, pair slot) half h, -1 pad
+    int32_t *loc_pos = nullptr;   // [2*KP][DVN][T] non-local edge u's LDS words, h=0 | h=1 << 16
+    int32_t *loc_info = nullptr;  // [2*KP][T] bit u + 4h: edge u present; bits 8+2h: local edge index
 };
+
+// Local-edge layout (loc_layout.cpp): see the comment there.
+constexpr int kLocMaxD = 8, kLocMaxCls = 4;
+struct LocLayout {
+    int T = 1024, KP = 0, DVN = 0, P = 0, ncls = 0, words = 0;
+    int DVN0 = 0, DVN1 = 0;     // non-local edges per variable of local slot 0 / 1 (max)
+    bool ABS0 = false, ABS1 = false;  // some variable of that slot has fewer
+    long conflicts = 0;  // sum over (instruction, half wave) of the busiest bank's extra lanes
+    int cls_q[kLocMaxCls + 1] = {0}, cls_d[kLocMaxCls] = {0}, cls_w[kLocMaxCls + 1] = {0};
+    std::vector<int32_t> var, pos, info;
+};
+bool build_loc_layout(int n, int m, const std::vector<int32_t> &cptr, const std::vector<int32_t> &cvar,
+                      const std::vector<int32_t> &vptr, const std::vector<int32_t> &vslot, LocLayout &L);
 
 // Irregular kernel (bp_irr_kernel): 1024 threads; LDS room for messages (bytes)
 // after the early-stop syndrome bits and the Monte-Carlo curve.

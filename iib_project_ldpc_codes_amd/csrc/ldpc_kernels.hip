@@ -49,6 +49,12 @@ constexpr int kWave = 64;
 #ifndef LDPC_SPA_RWIRE
 #define LDPC_SPA_RWIRE 1  // bp_lds_kernel sum-product: v->c wire = the clamped ratio R itself (see ratio_wire)
 #endif
+#ifndef LDPC_LOC_VGROUP
+#define LDPC_LOC_VGROUP 1  // bp_loc_kernel: variable pairs per scheduling group (0: no barriers)
+#endif
+#ifndef LDPC_LOC_CGROUP
+#define LDPC_LOC_CGROUP 1  // bp_loc_kernel: check pairs per scheduling group (0: no barriers)
+#endif
 #ifndef LDPC_CHECK_W64
 #define LDPC_CHECK_W64 0  // check phase writes each pair edge with its own ds_write_b64
 #endif
@@ -690,6 +696,12 @@ __device__ __forceinline__ float v2c_wire(float x) {
     if (ALGO == 0) return copysignf(1.0f - __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x), 0.0f, 23.0f)), x);
     return x;
 }
+// R-wire of the irregular kernel: the clamped ratio 2^x (check_update<0, D, true> input)
+template <int ALGO>
+__device__ __forceinline__ float v2c_rwire(float x) {
+    if (ALGO == 0) return __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(x, -23.0f, 23.0f));
+    return x;
+}
 template <int ALGO>
 __device__ __forceinline__ float2 v2c_wire2(float2 x) {
     if (ALGO == 0) {
@@ -730,34 +742,45 @@ __device__ __forceinline__ float2 ratio_wire2(float2 R) {
     return lo - u;
 }
 
-// Check-node update over D messages in registers; entries i >= d are padding
-// (+inf for min-sum, unit factors for sum-product).  Same product / min order as
-// oracle check_update_{spa,ms}: min-sum is bit-exact with it, sum-product agrees
-// to the stated tolerance.
+// a * b + c per lane as one v_pk_fma_f32 (the SLP vectoriser packs only some)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
+    const f32x2 r = __builtin_elementwise_fma(f32x2{a.x, a.y}, f32x2{b.x, b.y}, f32x2{c.x, c.y});
+    return make_float2(r.x, r.y);
+}
+
+// Check-node update over D messages in registers; entries i >= d are padding (+inf
+// for min-sum; skipped by sum-product).  Min-sum is bit-exact with oracle
+// check_update_ms; sum-product agrees with the oracle's exact rule to the stated
+// tolerance.
 template <int ALGO, int D, bool WIRE = false>
 __device__ __forceinline__ void check_update(float (&x)[D], float alpha, int d = D) {
     if (ALGO == 0) {
-        // (a_i, b_i) pairs live in float2 so both product chains are
-        // v_pk_mul_f32 (two lanes of work per VALU issue).
-        float2 ab[D];
+        // elementary-symmetric form (check_update_spa_pair_rwire) on the d inputs' ratios
+        // R = 2^x (WIRE: the ratios themselves), outputs log2 of the exclusive ratio; (E, O)
+        // sums in float2 so both chains are packed ops.  Entries i >= d are skipped.
+        float R[D];
 #pragma unroll
-        for (int i = 0; i < D; ++i) {
-            const float a = WIRE ? x[i]
-                                 : copysignf(1.0f - __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x[i]), 0.0f, 23.0f)), x[i]);
-            ab[i] = i < d ? make_float2(a, 2.0f - fabsf(a)) : make_float2(1.0f, 1.0f);
+        for (int i = 0; i < D; ++i)
+            R[i] = WIRE ? x[i] : __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(x[i], -23.0f, 23.0f));
+        float2 pre[D];  // (E, O) of inputs {0 .. i-1}
+        pre[0] = make_float2(1.0f, 0.0f);
+#pragma unroll
+        for (int i = 1; i < D; ++i) {
+            const float2 nx = pk_fma(make_float2(R[i - 1], R[i - 1]), make_float2(pre[i - 1].y, pre[i - 1].x), pre[i - 1]);
+            pre[i] = i - 1 < d ? nx : pre[i - 1];
         }
-        float2 pre[D], suf[D];
-        pre[0] = make_float2(1.0f, 1.0f);
+        const bool odd = (d - 1) & 1;
+        float2 suf = make_float2(1.0f, 0.0f);  // (E, O) of inputs {j+1 .. d-1}
 #pragma unroll
-        for (int i = 1; i < D; ++i) pre[i] = pre[i - 1] * ab[i - 1];
-        suf[D - 1] = make_float2(1.0f, 1.0f);
-#pragma unroll
-        for (int i = D - 2; i >= 0; --i) suf[i] = suf[i + 1] * ab[i + 1];
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            const float N = pre[i].x * suf[i].x;  // D_i +- N_i fused as in check_update_spa_pair
-            const float P = fmaf(pre[i].y, suf[i].y, N), Q = fmaf(pre[i].y, suf[i].y, -N);
-            x[i] = __builtin_amdgcn_logf(P * __builtin_amdgcn_rcpf(Q));
+        for (int j = D - 1; j >= 0; --j) {
+            if (j < d) {
+                const float E = fmaf(pre[j].x, suf.x, pre[j].y * suf.y), O = fmaf(pre[j].x, suf.y, pre[j].y * suf.x);
+                const float num = odd ? O : E, den = odd ? E : O;
+                const float2 ns = pk_fma(make_float2(R[j], R[j]), make_float2(suf.y, suf.x), suf);
+                x[j] = __builtin_amdgcn_logf(num * __builtin_amdgcn_rcpf(den));
+                suf = ns;
+            }
         }
     } else {
         // branch-free: m1 = running min, m2 = running second smallest (with
@@ -821,12 +844,6 @@ __device__ __forceinline__ void check_update_ms6(float (&x)[6], float alpha) {
     }
 }
 
-// a * b + c per lane as one v_pk_fma_f32 (the SLP vectoriser packs only some)
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float2 pk_fma(float2 a, float2 b, float2 c) {
-    const f32x2 r = __builtin_elementwise_fma(f32x2{a.x, a.y}, f32x2{b.x, b.y}, f32x2{c.x, c.y});
-    return make_float2(r.x, r.y);
-}
 
 // LOG = false (product-domain variable phase, bp_lds_kernel's PROD): the output
 // is the ratio (D+N)/(D-N) itself, i.e. 2^message; the log moves to the variable
@@ -880,11 +897,18 @@ __device__ __forceinline__ void check_update_spa_pair(float2 (&a)[D]) {
 // the cost of the ratio form's two product chains -- and two disjoint sets combine as
 // (E_a E_b + O_a O_b, E_a O_b + O_a E_b).  Magnitudes: E >= 1, O >= sum R >= 2^-23,
 // e_k < 2^(23 k + 3) <= 2^118 for the 5 inputs of a degree-6 check.
-template <int D>
+// INVX: the .x check has one input less, padded with R = 0 (E, O unchanged, but the
+// exclusive sets count one more input), so its outputs take the other parity's ratio.
+template <int D, bool INVX = false>
 __device__ __forceinline__ void check_update_spa_pair_rwire(float2 (&R)[D]) {
     const float2 one = make_float2(1.0f, 1.0f);
     auto ratio = [](float2 E, float2 O) {
-        if constexpr ((D - 1) % 2 == 1) return O * make_float2(__builtin_amdgcn_rcpf(E.x), __builtin_amdgcn_rcpf(E.y));
+        constexpr bool odd = (D - 1) % 2 == 1;
+        if constexpr (INVX) {
+            return odd ? make_float2(E.x * __builtin_amdgcn_rcpf(O.x), O.y * __builtin_amdgcn_rcpf(E.y))
+                       : make_float2(O.x * __builtin_amdgcn_rcpf(E.x), E.y * __builtin_amdgcn_rcpf(O.y));
+        }
+        if constexpr (odd) return O * make_float2(__builtin_amdgcn_rcpf(E.x), __builtin_amdgcn_rcpf(E.y));
         else return E * make_float2(__builtin_amdgcn_rcpf(O.x), __builtin_amdgcn_rcpf(O.y));
     };
     float2 pE[D], pO[D];  // prefix sets {0 .. i-1}
@@ -951,6 +975,10 @@ struct BpArgs {
     // irregular kernel layout (ldpc_graph::irr_*)
     const int32_t *irr_lane, *irr_cdeg;
     int irr_KC, irr_S, irr_P;
+    // local-edge kernel layout (ldpc_graph::loc_*)
+    const int32_t *loc_var, *loc_pos, *loc_info;
+    int loc_P, loc_ncls, loc_words;
+    int loc_cls_q[5], loc_cls_d[4], loc_cls_w[5];
 };
 
 // ---------------------------------------------------------------------------
@@ -1388,6 +1416,320 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// 2a'. Local-edge kernel (layout: loc_layout.cpp).  One codeword per workgroup of T
+//   threads; thread t updates check pairs q = t + kT (k < KP) and the four variables
+//   those checks hold as their local variables (var pairs 2k, 2k+1 on float2, .x = the
+//   pair's first check side).  The local edge of each variable -- one per variable --
+//   stays in a VGPR (loc[]) for the whole decode: the check phase reads it as input
+//   slot s of check pair k and overwrites it with the check's output; the variable
+//   phase reads that and overwrites it with the variable's extrinsic message.  Only the
+//   other E - n messages live in LDS (rows per degree class, lane-contiguous
+//   ds_read_b128 / ds_read_b64 on the check side, gathers on the variable side).
+//   Sum-product in the product domain as bp_lds_kernel (R-wire, elementary-symmetric
+//   check rule); min-sum in natural units, variable sums in variable_to_check_list order
+//   (the local edge spliced in at its index) so it stays bit-exact with the oracle.
+//   ABS: some variables have fewer than DVN+1 edges; their absent edges gather the
+//   neutral value (ratio 1 / sum 0) and write to a private dummy word.
+// ---------------------------------------------------------------------------
+template <int D, int ALGO, bool MIXED = false>
+__device__ __forceinline__ void loc_check_pair(float *msg, int W, int Nc, int i, float2 &l0, float2 &l1, float alpha) {
+    constexpr int U = D - 2;
+    float2 x[D];
+    x[0] = l0;
+    x[1] = l1;
+#pragma unroll
+    for (int r = 0; r < U / 2; ++r) {
+        const float4 f = *reinterpret_cast<const float4 *>(msg + W + r * 4 * Nc + 4 * i);
+        x[2 + 2 * r] = make_float2(f.x, f.y);
+        x[3 + 2 * r] = make_float2(f.z, f.w);
+    }
+    if constexpr (U % 2) x[D - 1] = *reinterpret_cast<const float2 *>(msg + W + (U / 2) * 4 * Nc + 2 * i);
+    if constexpr (ALGO == 0) {
+        if constexpr (MIXED) {  // the .x check has D - 1 edges: pad input R = 0
+            x[D - 1].x = 0.0f;
+            check_update_spa_pair_rwire<D, true>(x);
+        } else {
+            check_update_spa_pair_rwire<D>(x);
+        }
+    } else {
+        float xa[D], xb[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) { xa[j] = x[j].x; xb[j] = x[j].y; }
+        if constexpr (MIXED) {  // pad: an infinite magnitude changes no minimum or sign
+            xa[D - 1] = __builtin_inff();
+            check_update<1, D>(xa, alpha);
+            check_update<1, D>(xb, alpha);
+        } else if constexpr (D == 6) {
+            check_update_ms6(xa, alpha);
+            check_update_ms6(xb, alpha);
+        } else {
+            check_update<1, D>(xa, alpha);
+            check_update<1, D>(xb, alpha);
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) x[j] = make_float2(xa[j], xb[j]);
+    }
+#pragma unroll
+    for (int r = 0; r < U / 2; ++r)
+        *reinterpret_cast<float4 *>(msg + W + r * 4 * Nc + 4 * i) =
+            make_float4(x[2 + 2 * r].x, x[2 + 2 * r].y, x[3 + 2 * r].x, x[3 + 2 * r].y);
+    if constexpr (U % 2) *reinterpret_cast<float2 *>(msg + W + (U / 2) * 4 * Nc + 2 * i) = x[D - 1];
+    l0 = x[0];
+    l1 = x[1];
+}
+
+// code = dy, or dy | dx << 8 for a mixed pair (dx = dy - 1 = DHI - 1 only)
+template <int D, int DHI, int ALGO>
+__device__ __forceinline__ void loc_check_dispatch(int code, float *msg, int W, int Nc, int i, float2 &l0, float2 &l1,
+                                                   float alpha) {
+    if constexpr (D == DHI) {
+        if (code >> 8) loc_check_pair<D, ALGO, true>(msg, W, Nc, i, l0, l1, alpha);
+        else loc_check_pair<D, ALGO>(msg, W, Nc, i, l0, l1, alpha);
+    } else {
+        if (code == D) loc_check_pair<D, ALGO>(msg, W, Nc, i, l0, l1, alpha);
+        else loc_check_dispatch<D + 1, DHI, ALGO>(code, msg, W, Nc, i, l0, l1, alpha);
+    }
+}
+
+// a load whose index the compiler may not hoist out of the codeword loop (it would keep
+// one 64-bit address per load live across the decode -- VGPRs the loop needs)
+template <typename V>
+__device__ __forceinline__ V ld_fresh(const V *p, int idx) {
+    asm volatile("" : "+v"(idx));
+    return p[idx];
+}
+
+template <int N> using int_c = std::integral_constant<int, N>;
+template <bool B> using bool_c = std::integral_constant<bool, B>;
+
+// DVN0 / DVN1: non-local edges per variable of local slot 0 / 1 (max); ABS0 / ABS1: some
+// variable of that slot has fewer (its absent edges gather the neutral value).
+template <int DLO, int DHI, int DVN0, int DVN1, int KP, int T, int ALGO, bool ABS0, bool ABS1>
+__global__ __launch_bounds__(T) void bp_loc_kernel(BpArgs a) {
+    constexpr int VP = 2 * KP;  // variable pairs per thread
+    constexpr int DVM = DVN0 > DVN1 ? DVN0 : DVN1;
+    constexpr int DVA = DVM > 0 ? DVM : 1;
+    constexpr int DVP = DVA;  // rows of loc_pos per var pair
+    extern __shared__ __align__(16) unsigned char smem[];
+    float *msg = reinterpret_cast<float *>(smem);
+    const int tid = threadIdx.x;
+    const int n = a.n, iters = a.max_iters;
+    const int lpos0 = (int)((uint32_t)(size_t)(lds_u8 *)smem >> 2);
+    const uint32_t base2 = (uint32_t)lpos0 | ((uint32_t)lpos0 << 16);
+    constexpr bool SPA = ALGO == 0;
+    constexpr bool INF0 = ABS0 || ALGO == 1, INF1 = ABS1 || ALGO == 1;
+    uint32_t sp[VP][DVA];
+    uint32_t inf[VP];
+    auto dvn_of = [](auto s_tag) { return decltype(s_tag)::value ? DVN1 : DVN0; };
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+#pragma unroll
+        for (int u = 0; u < DVN0; ++u) sp[2 * k][u] = (uint32_t)a.loc_pos[((2 * k) * DVP + u) * T + tid] + base2;
+#pragma unroll
+        for (int u = 0; u < DVN1; ++u) sp[2 * k + 1][u] = (uint32_t)a.loc_pos[((2 * k + 1) * DVP + u) * T + tid] + base2;
+        if constexpr (INF0) inf[2 * k] = (uint32_t)a.loc_info[(2 * k) * T + tid];
+        if constexpr (INF1) inf[2 * k + 1] = (uint32_t)a.loc_info[(2 * k + 1) * T + tid];
+    }
+    (void)dvn_of;
+    auto at = [](uint32_t ba) -> lds_f32 & { return *(lds_f32 *)(size_t)ba; };
+    const float neutral = SPA ? 1.0f : 0.0f;
+
+    // gather the non-local c->v messages of var pair v (slot s) into cv[0 .. DN-1]
+    auto gather = [&](auto dn_tag, auto abs_tag, int v, float2 (&cv)[DVA], uint32_t (&a0)[DVA], uint32_t (&a1)[DVA]) {
+        constexpr int DN = decltype(dn_tag)::value;
+        constexpr bool AB = decltype(abs_tag)::value;
+#pragma unroll
+        for (int u = 0; u < DN; ++u) {
+            a0[u] = pos_lo_x4(sp[v][u]);
+            a1[u] = pos_hi_x4(sp[v][u]);
+        }
+#pragma unroll
+        for (int u = 0; u < DN; ++u) cv[u] = make_float2(at(a0[u]), at(a1[u]));
+        if constexpr (AB) {
+#pragma unroll
+            for (int u = 0; u < DN; ++u) {
+                cv[u].x = (inf[v] >> u) & 1u ? cv[u].x : neutral;
+                cv[u].y = (inf[v] >> (u + 4)) & 1u ? cv[u].y : neutral;
+            }
+        }
+    };
+    // min-sum posterior of var pair v: L + messages in variable_to_check_list order,
+    // the local one spliced in at its index jl (the oracle's order: bit-exact)
+    auto ms_sum = [&](auto dn_tag, int v, const float2 &Lv, const float2 &lv, const float2 (&cv)[DVA]) {
+        constexpr int DN = decltype(dn_tag)::value;
+        float s2[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int jl = (inf[v] >> (8 + 2 * h)) & 3;
+            const float ml = h ? lv.y : lv.x;
+            float s = h ? Lv.y : Lv.x;
+#pragma unroll
+            for (int j = 0; j <= DN; ++j) {
+                const float nl = j == 0 ? 0.0f : (h ? cv[j - 1].y : cv[j - 1].x);
+                const float nl2 = j < DN ? (h ? cv[j].y : cv[j].x) : 0.0f;
+                s += j < jl ? nl2 : (j == jl ? ml : nl);
+            }
+            s2[h] = s;
+        }
+        return make_float2(s2[0], s2[1]);
+    };
+
+    for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+        __syncthreads();  // the previous codeword's outputs are out of LDS
+        for (int v = tid; v < n; v += T) msg[v] = a.llr[(size_t)b * n + v] * Domain<ALGO>::in;
+        __syncthreads();
+        float2 L[VP];  // SPA: E = 2^channel (clamped); min-sum: channel LLR
+#pragma unroll
+        for (int v = 0; v < VP; ++v) {
+            const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid), v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
+            L[v] = make_float2(v0 >= 0 ? msg[v0] : 0.0f, v1 >= 0 ? msg[v1] : 0.0f);
+        }
+        __syncthreads();
+        float2 loc[VP];
+        auto init = [&](auto dn_tag, int v) {
+            constexpr int DN = decltype(dn_tag)::value;
+            float2 w;
+            if constexpr (SPA) {
+                w = make_float2(__builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].x, -23.0f, 23.0f)),
+                                __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].y, -23.0f, 23.0f)));
+                L[v] = make_float2(__builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].x, -126.0f, 126.0f)),
+                                   __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].y, -126.0f, 126.0f)));
+            } else {
+                w = L[v];
+            }
+            loc[v] = w;
+#pragma unroll
+            for (int u = 0; u < DN; ++u) {
+                at(pos_lo_x4(sp[v][u])) = w.x;
+                at(pos_hi_x4(sp[v][u])) = w.y;
+            }
+        };
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            init(int_c<DVN0>{}, 2 * k);
+            init(int_c<DVN1>{}, 2 * k + 1);
+        }
+        // variable phase of var pair v
+        auto var_pair = [&](auto dn_tag, auto abs_tag, int v) {
+            constexpr int DN = decltype(dn_tag)::value;
+            constexpr int DV = DN + 1;
+            uint32_t a0[DVA], a1[DVA];
+            float2 cv[DVA];
+            gather(dn_tag, abs_tag, v, cv, a0, a1);
+            if constexpr (SPA) {
+                // edges e_0 = local, e_{1+u} = non-local u: R_j = E prod_{k != j} e_k
+                float2 pre[DV];
+                pre[0] = L[v];
+                if constexpr (DV > 1) pre[1] = pre[0] * loc[v];
+#pragma unroll
+                for (int j = 2; j < DV; ++j) pre[j] = pre[j - 1] * cv[j - 2];
+                float2 suf = DN > 0 ? cv[DN > 0 ? DN - 1 : 0] : make_float2(1.0f, 1.0f);
+#pragma unroll
+                for (int j = DV - 1; j >= 1; --j) {
+                    const float2 R = ratio_wire2(j == DV - 1 ? pre[j] : pre[j] * suf);
+                    at(a0[j - 1]) = R.x;
+                    at(a1[j - 1]) = R.y;
+                    if (j < DV - 1) suf = suf * cv[j - 1];
+                }
+                loc[v] = ratio_wire2(DN > 0 ? L[v] * suf : L[v]);
+            } else {
+                const float2 s = ms_sum(dn_tag, v, L[v], loc[v], cv);
+#pragma unroll
+                for (int u = 0; u < DN; ++u) {
+                    at(a0[u]) = s.x - cv[u].x;
+                    at(a1[u]) = s.y - cv[u].y;
+                }
+                loc[v] = make_float2(s.x - loc[v].x, s.y - loc[v].y);
+            }
+        };
+        for (int it = 0; it < iters; ++it) {
+            __syncthreads();  // variable phase (or initialisation) complete
+            // ---- check phase ----
+#pragma unroll
+            for (int k = 0; k < KP; ++k) {
+                int q = tid + k * T;
+                asm volatile("" : "+v"(q));  // recomputed per iteration: no per-pair addresses held live
+                if (q < (LDPC_ABLATE_PHASE == 1 ? 0 : a.loc_P)) {
+                    if constexpr (DLO == DHI) {  // one class: rows of P pairs from word 0
+                        loc_check_pair<DLO, ALGO>(msg, 0, a.loc_P, q, loc[2 * k], loc[2 * k + 1], a.alpha);
+                    } else {
+                        // class of q by selects on the (scalar) class table -- no per-lane
+                        // indexing of kernel arguments
+                        int q0 = a.loc_cls_q[0], q1 = a.loc_cls_q[1], W = a.loc_cls_w[0], d = a.loc_cls_d[0];
+#pragma unroll
+                        for (int j = 1; j < 4; ++j) {
+                            const bool in = j < a.loc_ncls && q >= a.loc_cls_q[j];
+                            q0 = in ? a.loc_cls_q[j] : q0;
+                            q1 = in ? a.loc_cls_q[j + 1] : q1;
+                            W = in ? a.loc_cls_w[j] : W;
+                            d = in ? a.loc_cls_d[j] : d;
+                        }
+                        loc_check_dispatch<DLO, DHI, ALGO>(d, msg, W, q1 - q0, q - q0, loc[2 * k], loc[2 * k + 1],
+                                                           a.alpha);
+                    }
+                }
+                if (LDPC_LOC_CGROUP > 0 && k % LDPC_LOC_CGROUP == LDPC_LOC_CGROUP - 1)
+                    __builtin_amdgcn_sched_barrier(0);  // pairs in flight (VGPR budget)
+            }
+            __syncthreads();
+            if (it == iters - 1) break;  // the last variable phase only forms posteriors
+            // ---- variable phase ----
+            if constexpr (LDPC_ABLATE_PHASE != 2) {
+#pragma unroll
+                for (int k = 0; k < KP; ++k) {
+                    var_pair(int_c<DVN0>{}, bool_c<ABS0>{}, 2 * k);
+                    if (LDPC_LOC_VGROUP == 1) __builtin_amdgcn_sched_barrier(0);
+                    var_pair(int_c<DVN1>{}, bool_c<ABS1>{}, 2 * k + 1);
+                    if (LDPC_LOC_VGROUP > 0) __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        // ---- posteriors (after the last check phase) and outputs ----
+        // (variable ids re-read where needed: not kept live through the decode loop)
+        float2 pr[VP];
+        auto post = [&](auto dn_tag, auto abs_tag, int v) {
+            constexpr int DN = decltype(dn_tag)::value;
+            uint32_t a0[DVA], a1[DVA];
+            float2 cv[DVA];
+            gather(dn_tag, abs_tag, v, cv, a0, a1);
+            if constexpr (SPA) {
+                const float *lb = a.llr + (size_t)b * n;
+                const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid), v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
+                float2 s = make_float2(v0 >= 0 ? ld_fresh(lb, v0) * Domain<ALGO>::in : 0.0f,
+                                       v1 >= 0 ? ld_fresh(lb, v1) * Domain<ALGO>::in : 0.0f);
+                s = s + make_float2(__builtin_amdgcn_logf(loc[v].x), __builtin_amdgcn_logf(loc[v].y));
+#pragma unroll
+                for (int u = 0; u < DN; ++u)
+                    s = s + make_float2(__builtin_amdgcn_logf(cv[u].x), __builtin_amdgcn_logf(cv[u].y));
+                pr[v] = s;
+            } else {
+                pr[v] = ms_sum(dn_tag, v, L[v], loc[v], cv);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // one var pair's gathers in flight (VGPR budget)
+        };
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            post(int_c<DVN0>{}, bool_c<ABS0>{}, 2 * k);
+            post(int_c<DVN1>{}, bool_c<ABS1>{}, 2 * k + 1);
+        }
+        __syncthreads();  // all gathers done before the staging overwrites messages
+#pragma unroll
+        for (int v = 0; v < VP; ++v) {
+            const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid), v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
+            if (v0 >= 0) msg[v0] = pr[v].x;
+            if (v1 >= 0) msg[v1] = pr[v].y;
+        }
+        __syncthreads();
+        for (int v = tid; v < n; v += T) {
+            const float s = msg[v];
+            if (a.post) a.post[(size_t)b * n + v] = s * Domain<ALGO>::out;
+            if (a.hard) a.hard[(size_t)b * n + v] = (uint8_t)(s < 0.0f);
+        }
+        if (a.its && tid == 0) a.its[b] = iters;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // 2b. Generic path: any (irregular) CSR graph, check degree <= MAXDC.
 //   Messages in LDS when they fit, else in a per-workgroup global scratch
 //   slab (GMEM; the slab stays L2 / Infinity-Cache resident).  Channel LLRs
@@ -1580,7 +1922,7 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
 //   check c = k*1024 + t is thread t's row-k check; its slot j sits at position
 //   (k*DC + j)*1024 + t, so a row's reads and writes are lane-contiguous (LDS
 //   conflict-free, coalesced in the slab).  Absent slots (degree < DC) hold the
-//   rule's neutral input (sum-product wire a = 1, min-sum +inf) and are never
+//   rule's neutral input (min-sum +inf; sum-product skips them by degree) and are never
 //   written, so the update runs on DC entries without a degree test (x1 and
 //   min(+inf, .) change nothing: same values as oracle check_update_*(x, d)).
 //   Positions [0, S) are in LDS, [S, P) in a per-workgroup global slab (whole
@@ -1644,7 +1986,7 @@ __global__ __launch_bounds__(kIrrT) void bp_irr_kernel(BpArgs a) {
             if (v >= 0) l = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
             err0 += (v >= 0) & (l < 0.0f);
             L[i] = l * Domain<ALGO>::in;
-            const float w = v2c_wire<ALGO>(L[i]);
+            const float w = v2c_rwire<ALGO>(L[i]);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 if (__builtin_amdgcn_readfirstlane(POS(i, j)) != 0xFFFFu) ST(POS(i, j), w);
@@ -1694,7 +2036,7 @@ __global__ __launch_bounds__(kIrrT) void bp_irr_kernel(BpArgs a) {
                     if constexpr (!FINAL) {
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
-                            if (has[u][j]) ST(POS(i, j), v2c_wire<ALGO>(s - cv[u][j]));
+                            if (has[u][j]) ST(POS(i, j), v2c_rwire<ALGO>(s - cv[u][j]));
                     }
                     if constexpr (ET) {
                         if (s < 0.0f) {
@@ -1739,7 +2081,7 @@ __global__ __launch_bounds__(kIrrT) void bp_irr_kernel(BpArgs a) {
                     for (int j = 0; j < DC; ++j) x[j] = slab[q0 + j * T];
                 }
                 if constexpr (ALGO == 1 && DC == 6) check_update_ms6(x, a.alpha);
-                else check_update<ALGO, DC, true>(x, a.alpha);
+                else check_update<ALGO, DC, true>(x, a.alpha, d);
                 if (in_lds) {
 #pragma unroll
                     for (int j = 0; j < DC; ++j)
@@ -2701,7 +3043,29 @@ BecArgs bec_args(const ldpc_graph &g) {
 }
 
 // --- soft path selection ---------------------------------------------------
-enum class BpPath { Lds36, Irr, Generic8, Generic16, Generic32, GenericG8, GenericG16, GenericG32, None };
+enum class BpPath { Loc, Lds36, Irr, Generic8, Generic16, Generic32, GenericG8, GenericG16, GenericG32, None };
+
+#ifndef LDPC_LOC
+#define LDPC_LOC 1  // fixed-count decode on bp_loc_kernel when the graph has a local-edge layout
+#endif
+// bp_loc_kernel shapes: (check-degree range, non-local edges per variable, absent edges)
+// x (threads, check pairs per thread)
+bool loc_shape(const ldpc_graph &g, int &T, int &KP) {
+    if (!g.loc_KP) return false;
+    // (3,6): both slots 2 non-local edges, none absent; RSU-type rate-1/2 ensembles with
+    // variable degrees 2..4 and check degrees 5..6: slot 0 a degree-2 variable
+    const bool reg36 = g.loc_dlo == 6 && g.loc_dhi == 6 && g.loc_DVN == 2 && g.loc_dvn0 == 2 && g.loc_dvn1 == 2 &&
+                       !g.loc_abs0 && !g.loc_abs1;
+    const bool rsu = g.loc_dlo >= 5 && g.loc_dhi == 6 && g.loc_DVN == 3 && g.loc_dvn0 == 1 && !g.loc_abs0;
+    if (!reg36 && !rsu) return false;
+    T = g.loc_T;
+    KP = g.loc_KP;
+    return (T == 256 && KP >= 1 && KP <= 4) || (T == 1024 && KP >= 2 && KP <= 3) ||
+           (T == 512 && (KP == 8 || KP == 10) && rsu);
+}
+size_t loc_lds_bytes(const ldpc_graph &g) {
+    return ((size_t)std::max(g.loc_words + 64, g.n) * 4 + 15) & ~(size_t)15;
+}
 
 // bp_irr_kernel: LDS bytes (messages, syndrome bits, curve) and whether the slab is used
 size_t irr_lds_bytes(const ldpc_graph &g, int iters) {
@@ -2724,6 +3088,9 @@ size_t generic_lds_bytes(const ldpc_graph &g, int iters, bool mc) {
 
 BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc) {
     if (!g.consistent) return BpPath::None;
+    int lT = 0, lKP = 0;
+    if (LDPC_LOC && !et && !mc && iters > 0 && loc_shape(g, lT, lKP) && loc_lds_bytes(g) <= kLdsMax - 2048)
+        return BpPath::Loc;
     if (g.lane_var && g.dv == 3 && g.dc == 6 && lds36_bytes(g, iters, et, mc) <= kLdsMax - 2048)
         return BpPath::Lds36;
     if (g.irr_lane && irr_lds_bytes(g, iters) <= kLdsMax - 1024) return BpPath::Irr;
@@ -2792,6 +3159,52 @@ hipError_t launch_generic(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int DLO, int DHI, int D0, int D1, bool A0, bool A1, int T, int KP, int ALGO>
+hipError_t launch_loc_shape(const ldpc_graph &g, const BpArgs &a, hipStream_t s) {
+    auto k = bp_loc_kernel<DLO, DHI, D0, D1, KP, T, ALGO, A0, A1>;
+    const size_t lds = loc_lds_bytes(g);
+    hipError_t e = allow_lds(k, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(a.B), dim3(T), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int DLO, int DHI, int D0, int D1, bool A0, bool A1, int ALGO>
+hipError_t launch_loc_deg(const ldpc_graph &g, const BpArgs &a, int T, int KP, hipStream_t s) {
+    if (T == 256) {
+        if (KP == 1) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 256, 1, ALGO>(g, a, s);
+        if (KP == 2) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 256, 2, ALGO>(g, a, s);
+        if (KP == 3) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 256, 3, ALGO>(g, a, s);
+        if (KP == 4) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 256, 4, ALGO>(g, a, s);
+    } else if (T == 1024) {
+        if (KP == 2) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 1024, 2, ALGO>(g, a, s);
+        if (KP == 3) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 1024, 3, ALGO>(g, a, s);
+    } else if constexpr (DLO != DHI) {  // 512 threads, 2 waves per SIMD: the RSU-type shape only
+        if (KP == 8) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 512, 8, ALGO>(g, a, s);
+        if (KP == 10) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 512, 10, ALGO>(g, a, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int ALGO>
+hipError_t launch_loc(const ldpc_graph &g, BpArgs a, hipStream_t s) {
+    int T = 0, KP = 0;
+    if (!loc_shape(g, T, KP)) return hipErrorInvalidValue;
+    a.loc_var = g.loc_var;
+    a.loc_pos = g.loc_pos;
+    a.loc_info = g.loc_info;
+    a.loc_P = g.loc_P;
+    a.loc_ncls = g.loc_ncls;
+    a.loc_words = g.loc_words;
+    for (int i = 0; i < 5; ++i) {
+        a.loc_cls_q[i] = g.loc_cls_q[i];
+        a.loc_cls_w[i] = g.loc_cls_w[i];
+    }
+    for (int i = 0; i < 4; ++i) a.loc_cls_d[i] = g.loc_cls_d[i];
+    if (g.loc_dlo == 6) return launch_loc_deg<6, 6, 2, 2, false, false, ALGO>(g, a, T, KP, s);
+    return launch_loc_deg<5, 6, 1, 3, false, true, ALGO>(g, a, T, KP, s);
+}
+
 template <int DC, int VPT, int ALGO, bool ET, bool MC>
 hipError_t launch_irr_shape(const ldpc_graph &g, const BpArgs &a, hipStream_t s) {
     auto k = bp_irr_kernel<DC, VPT, ALGO, ET, MC>;
@@ -2821,6 +3234,9 @@ hipError_t launch_irr(const ldpc_graph &g, BpArgs a, hipStream_t s) {
 template <int ALGO, bool ET, bool MC>
 hipError_t dispatch_bp(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     switch (choose_path(g, a.max_iters, ET, MC)) {
+        case BpPath::Loc:
+            if constexpr (!ET && !MC) return launch_loc<ALGO>(g, a, s);
+            return hipErrorInvalidValue;
         case BpPath::Lds36: return launch_lds36<ALGO, ET, MC>(g, a, s);
         case BpPath::Irr: return launch_irr<ALGO, ET, MC>(g, a, s);
         case BpPath::Generic8: return launch_generic<8, ALGO, ET, MC, false>(g, a, s);
@@ -2893,6 +3309,7 @@ size_t bp_scratch_bytes(const ldpc_graph &g, int B) {
 
 const char *bp_kernel_name(const ldpc_graph &g, int early_stop) {
     switch (choose_path(g, 50, early_stop != 0, false)) {
+        case BpPath::Loc: return "bp_loc_kernel";
         case BpPath::Lds36: return "bp_lds_kernel<3,6>";
         case BpPath::Irr: return irr_slab(g) ? "bp_irr_kernel<lds+slab>" : "bp_irr_kernel<lds>";
         case BpPath::Generic8: return "bp_generic_kernel<8,lds>";

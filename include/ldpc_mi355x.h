@@ -295,6 +295,18 @@ int ldpc_debug_lane_layout(const int32_t *variable_to_check_list, const int32_t 
 int ldpc_debug_irr_layout(const int32_t *check_ptr, const int32_t *check_var, const int32_t *var_ptr,
                           const int32_t *var_slot, int n, int m, int32_t *shape, int32_t *lane, int32_t *cdeg);
 
+/*
+ * Host-only: the local-edge layout of bp_loc_kernel for a CSR graph (no device
+ * needed; tests / diagnostics).  shape: int32[24] = {T, KP, DVN, P, words, classes,
+ * bank-conflict cost, cls_q[5], cls_d[4], cls_w[5], DVN0 | ABS0 << 8, DVN1 | ABS1 << 8}; var: int32[2*KP*2*T] variable
+ * ids, pos: int32[2*KP*max(DVN,1)*T] packed LDS words, info: int32[2*KP*T] (see
+ * ldpc_graph::loc_* in csrc/ldpc_internal.hpp).  NULL arrays: shape only.  Returns
+ * LDPC_EUNSUP when the graph has no such layout.
+ */
+int ldpc_debug_loc_layout(const int32_t *check_ptr, const int32_t *check_var, const int32_t *var_ptr,
+                          const int32_t *var_slot, int n, int m, int T, int32_t *shape, int32_t *var, int32_t *pos,
+                          int32_t *info);
+
 /* Name of the soft kernel a graph dispatches to (tests / bench). */
 const char *ldpc_bp_kernel_name(const ldpc_graph *g, int early_stop);
 

@@ -335,7 +335,7 @@ def test_headline_shape_spa_vs_oracle(torch):
     """(3,6) n=10000 (the bench workload's code) on a small batch."""
     from iib_project_ldpc_codes_amd import decoder
     g, csr, llr = _soft_case(10000, 8, 0.85, 15)
-    assert g.kernel_name().startswith("bp_lds_kernel")
+    assert g.kernel_name() in ("bp_loc_kernel", "bp_lds_kernel<3,6>")
     post, hard, its = decoder.bp_decode(g, llr, 3, "spa")
     opost, _, _ = oracle.bp_decode_batch(csr, llr, 3, 0)
     np.testing.assert_allclose(post, opost, rtol=SPA_RTOL, atol=SPA_ATOL)
