@@ -125,17 +125,22 @@ def cpu_baseline(graph, llr_host, seconds):
     used = []
 
     def bec(threads, secs):
+        if kind == "reference":
+            # a fresh interpreter (no torch / HIP runtime threads): the reference's C on the
+            # host cores exactly as a CPU-only run would use them
+            import multiprocessing as mp
+            with mp.get_context("spawn").Pool(1) as pool:
+                done, el, u = pool.apply(oracle.ref_bench_timed, (words, 50, gb.check_lookup, gb.variable_lookup,
+                                                                  gb.n, gb.k, DV, DC, threads, secs))
+            used.append(u)
+            return done, el
+        oracle.set_num_threads(threads)
         chunk = 64 * threads
 
         def fn(i):
             lo = (i * chunk) % words.shape[0]
             sl = words[lo:lo + chunk] if lo + chunk <= words.shape[0] else words[:chunk]
-            if kind == "reference":
-                used.append(oracle.ref_bench_message_passing(sl, 50, gb.check_lookup, gb.variable_lookup, gb.n,
-                                                             gb.k, DV, DC, threads)[3])
-            else:
-                oracle.set_num_threads(threads)
-                oracle.bec_decode_batch(sl, 50, gb.variable_lookup, gb.check_lookup, gb.n, gb.k, DV, DC)
+            oracle.bec_decode_batch(sl, 50, gb.variable_lookup, gb.check_lookup, gb.n, gb.k, DV, DC)
             return sl.shape[0]
         return _timed(fn, chunk, secs)
 

@@ -1431,8 +1431,12 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 //   ABS: some variables have fewer than DVN+1 edges; their absent edges gather the
 //   neutral value (ratio 1 / sum 0) and write to a private dummy word.
 // ---------------------------------------------------------------------------
-template <int D, int ALGO, bool MIXED = false>
-__device__ __forceinline__ void loc_check_pair(float *msg, int W, int Nc, int i, float2 &l0, float2 &l1, float alpha) {
+// SGN (sum-product with early stop): every v->c ratio carries its variable's hard
+// decision in the sign bit; the pair's parities of those bits are the syndrome of the
+// previous variable phase (returned: 1 = a check of the pair unsatisfied), then the
+// magnitudes are the ratios.
+template <int D, int ALGO, bool MIXED = false, bool SGN = false>
+__device__ __forceinline__ int loc_check_pair(float *msg, int W, int Nc, int i, float2 &l0, float2 &l1, float alpha) {
     constexpr int U = D - 2;
     float2 x[D];
     x[0] = l0;
@@ -1444,6 +1448,17 @@ __device__ __forceinline__ void loc_check_pair(float *msg, int W, int Nc, int i,
         x[3 + 2 * r] = make_float2(f.z, f.w);
     }
     if constexpr (U % 2) x[D - 1] = *reinterpret_cast<const float2 *>(msg + W + (U / 2) * 4 * Nc + 2 * i);
+    int unsat = 0;
+    if constexpr (SGN) {
+        uint32_t px = 0, py = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            px ^= __float_as_uint(x[j].x);
+            py ^= __float_as_uint(x[j].y);
+            x[j] = make_float2(fabsf(x[j].x), fabsf(x[j].y));
+        }
+        unsat = (int)((px | py) >> 31);
+    }
     if constexpr (ALGO == 0) {
         if constexpr (MIXED) {  // the .x check has D - 1 edges: pad input R = 0
             x[D - 1].x = 0.0f;
@@ -1476,18 +1491,19 @@ __device__ __forceinline__ void loc_check_pair(float *msg, int W, int Nc, int i,
     if constexpr (U % 2) *reinterpret_cast<float2 *>(msg + W + (U / 2) * 4 * Nc + 2 * i) = x[D - 1];
     l0 = x[0];
     l1 = x[1];
+    return unsat;
 }
 
 // code = dy, or dy | dx << 8 for a mixed pair (dx = dy - 1 = DHI - 1 only)
-template <int D, int DHI, int ALGO>
-__device__ __forceinline__ void loc_check_dispatch(int code, float *msg, int W, int Nc, int i, float2 &l0, float2 &l1,
-                                                   float alpha) {
+template <int D, int DHI, int ALGO, bool SGN>
+__device__ __forceinline__ int loc_check_dispatch(int code, float *msg, int W, int Nc, int i, float2 &l0, float2 &l1,
+                                                  float alpha) {
     if constexpr (D == DHI) {
-        if (code >> 8) loc_check_pair<D, ALGO, true>(msg, W, Nc, i, l0, l1, alpha);
-        else loc_check_pair<D, ALGO>(msg, W, Nc, i, l0, l1, alpha);
+        if (code >> 8) return loc_check_pair<D, ALGO, true, SGN>(msg, W, Nc, i, l0, l1, alpha);
+        return loc_check_pair<D, ALGO, false, SGN>(msg, W, Nc, i, l0, l1, alpha);
     } else {
-        if (code == D) loc_check_pair<D, ALGO>(msg, W, Nc, i, l0, l1, alpha);
-        else loc_check_dispatch<D + 1, DHI, ALGO>(code, msg, W, Nc, i, l0, l1, alpha);
+        if (code == D) return loc_check_pair<D, ALGO, false, SGN>(msg, W, Nc, i, l0, l1, alpha);
+        return loc_check_dispatch<D + 1, DHI, ALGO, SGN>(code, msg, W, Nc, i, l0, l1, alpha);
     }
 }
 
@@ -1504,8 +1520,13 @@ template <bool B> using bool_c = std::integral_constant<bool, B>;
 
 // DVN0 / DVN1: non-local edges per variable of local slot 0 / 1 (max); ABS0 / ABS1: some
 // variable of that slot has fewer (its absent edges gather the neutral value).
-template <int DLO, int DHI, int DVN0, int DVN1, int KP, int T, int ALGO, bool ABS0, bool ABS1>
+// MC (sum-product): fused Philox channel, per-iteration error counts of the all-zero
+// codeword into the trial curve, no posteriors; ET with MC: syndrome early stop on the
+// sign-bit decisions (see loc_check_pair).
+template <int DLO, int DHI, int DVN0, int DVN1, int KP, int T, int ALGO, bool ABS0, bool ABS1, bool ET = false,
+          bool MC = false>
 __global__ __launch_bounds__(T) void bp_loc_kernel(BpArgs a) {
+    static_assert(!ET || (MC && ALGO == 0), "early stop: sum-product Monte-Carlo only");
     constexpr int VP = 2 * KP;  // variable pairs per thread
     constexpr int DVM = DVN0 > DVN1 ? DVN0 : DVN1;
     constexpr int DVA = DVM > 0 ? DVM : 1;
@@ -1574,10 +1595,27 @@ __global__ __launch_bounds__(T) void bp_loc_kernel(BpArgs a) {
         return make_float2(s2[0], s2[1]);
     };
 
+    int *curve = reinterpret_cast<int *>(smem + (((size_t)(a.loc_words + 64 > n ? a.loc_words + 64 : n) * 4 + 15) &
+                                                  ~(size_t)15));
     for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+        const uint64_t cw = a.first_cw + (uint64_t)b;
         __syncthreads();  // the previous codeword's outputs are out of LDS
-        for (int v = tid; v < n; v += T) msg[v] = a.llr[(size_t)b * n + v] * Domain<ALGO>::in;
+        int err0 = 0;
+        if constexpr (MC) {
+            for (int i = tid; i <= iters; i += T) curve[i] = 0;
+            for (int v = tid; v < n; v += T) {
+                const float l = chan_soft(a.ch, cw, v);
+                msg[v] = l * Domain<ALGO>::in;
+                err0 += (l < 0.0f);
+            }
+        } else {
+            for (int v = tid; v < n; v += T) msg[v] = a.llr[(size_t)b * n + v] * Domain<ALGO>::in;
+        }
         __syncthreads();
+        if constexpr (MC) {
+            const int w = wave_sum(err0);
+            if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[0], w);
+        }
         float2 L[VP];  // SPA: E = 2^channel (clamped); min-sum: channel LLR
 #pragma unroll
         for (int v = 0; v < VP; ++v) {
@@ -1592,6 +1630,7 @@ __global__ __launch_bounds__(T) void bp_loc_kernel(BpArgs a) {
             if constexpr (SPA) {
                 w = make_float2(__builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].x, -23.0f, 23.0f)),
                                 __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].y, -23.0f, 23.0f)));
+                if constexpr (ET) w = make_float2(copysignf(w.x, L[v].x), copysignf(w.y, L[v].y));
                 L[v] = make_float2(__builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].x, -126.0f, 126.0f)),
                                    __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].y, -126.0f, 126.0f)));
             } else {
@@ -1609,13 +1648,14 @@ __global__ __launch_bounds__(T) void bp_loc_kernel(BpArgs a) {
             init(int_c<DVN0>{}, 2 * k);
             init(int_c<DVN1>{}, 2 * k + 1);
         }
-        // variable phase of var pair v
-        auto var_pair = [&](auto dn_tag, auto abs_tag, int v) {
+        // variable phase of var pair v; returns the pair's hard decisions (bit 0: .x, 1: .y)
+        auto var_pair = [&](auto dn_tag, auto abs_tag, int v) -> int {
             constexpr int DN = decltype(dn_tag)::value;
             constexpr int DV = DN + 1;
             uint32_t a0[DVA], a1[DVA];
             float2 cv[DVA];
             gather(dn_tag, abs_tag, v, cv, a0, a1);
+            int dec = 0;
             if constexpr (SPA) {
                 // edges e_0 = local, e_{1+u} = non-local u: R_j = E prod_{k != j} e_k
                 float2 pre[DV];
@@ -1623,15 +1663,29 @@ __global__ __launch_bounds__(T) void bp_loc_kernel(BpArgs a) {
                 if constexpr (DV > 1) pre[1] = pre[0] * loc[v];
 #pragma unroll
                 for (int j = 2; j < DV; ++j) pre[j] = pre[j - 1] * cv[j - 2];
+                uint32_t sx = 0, sy = 0;  // ET: the decision rides in every outgoing sign bit
+                if constexpr (MC) {
+                    const float2 P = DN > 0 ? pre[DV - 1] * cv[DN > 0 ? DN - 1 : 0] : pre[DV - 1];
+                    dec = (int)(P.x < 1.0f) | ((int)(P.y < 1.0f) << 1);
+                    if constexpr (ET) {
+                        sx = (uint32_t)(dec & 1) << 31;
+                        sy = (uint32_t)(dec >> 1) << 31;
+                    }
+                }
+                auto sgn = [&](float2 R) {
+                    if constexpr (ET) return make_float2(__uint_as_float(__float_as_uint(R.x) | sx),
+                                                         __uint_as_float(__float_as_uint(R.y) | sy));
+                    return R;
+                };
                 float2 suf = DN > 0 ? cv[DN > 0 ? DN - 1 : 0] : make_float2(1.0f, 1.0f);
 #pragma unroll
                 for (int j = DV - 1; j >= 1; --j) {
-                    const float2 R = ratio_wire2(j == DV - 1 ? pre[j] : pre[j] * suf);
+                    const float2 R = sgn(ratio_wire2(j == DV - 1 ? pre[j] : pre[j] * suf));
                     at(a0[j - 1]) = R.x;
                     at(a1[j - 1]) = R.y;
                     if (j < DV - 1) suf = suf * cv[j - 1];
                 }
-                loc[v] = ratio_wire2(DN > 0 ? L[v] * suf : L[v]);
+                loc[v] = sgn(ratio_wire2(DN > 0 ? L[v] * suf : L[v]));
             } else {
                 const float2 s = ms_sum(dn_tag, v, L[v], loc[v], cv);
 #pragma unroll
@@ -1641,9 +1695,12 @@ __global__ __launch_bounds__(T) void bp_loc_kernel(BpArgs a) {
                 }
                 loc[v] = make_float2(s.x - loc[v].x, s.y - loc[v].y);
             }
+            return dec;
         };
-        for (int it = 0; it < iters; ++it) {
+        int it = 0;
+        for (; it < iters; ++it) {
             __syncthreads();  // variable phase (or initialisation) complete
+            int unsat = 0;
             // ---- check phase ----
 #pragma unroll
             for (int k = 0; k < KP; ++k) {
@@ -1651,7 +1708,8 @@ __global__ __launch_bounds__(T) void bp_loc_kernel(BpArgs a) {
                 asm volatile("" : "+v"(q));  // recomputed per iteration: no per-pair addresses held live
                 if (q < (LDPC_ABLATE_PHASE == 1 ? 0 : a.loc_P)) {
                     if constexpr (DLO == DHI) {  // one class: rows of P pairs from word 0
-                        loc_check_pair<DLO, ALGO>(msg, 0, a.loc_P, q, loc[2 * k], loc[2 * k + 1], a.alpha);
+                        unsat |= loc_check_pair<DLO, ALGO, false, ET>(msg, 0, a.loc_P, q, loc[2 * k], loc[2 * k + 1],
+                                                                      a.alpha);
                     } else {
                         // class of q by selects on the (scalar) class table -- no per-lane
                         // indexing of kernel arguments
@@ -1664,25 +1722,45 @@ __global__ __launch_bounds__(T) void bp_loc_kernel(BpArgs a) {
                             W = in ? a.loc_cls_w[j] : W;
                             d = in ? a.loc_cls_d[j] : d;
                         }
-                        loc_check_dispatch<DLO, DHI, ALGO>(d, msg, W, q1 - q0, q - q0, loc[2 * k], loc[2 * k + 1],
-                                                           a.alpha);
+                        unsat |= loc_check_dispatch<DLO, DHI, ALGO, ET>(d, msg, W, q1 - q0, q - q0, loc[2 * k],
+                                                                        loc[2 * k + 1], a.alpha);
                     }
                 }
                 if (LDPC_LOC_CGROUP > 0 && k % LDPC_LOC_CGROUP == LDPC_LOC_CGROUP - 1)
                     __builtin_amdgcn_sched_barrier(0);  // pairs in flight (VGPR budget)
             }
-            __syncthreads();
-            if (it == iters - 1) break;  // the last variable phase only forms posteriors
+            if constexpr (ET) {
+                // the syndrome of the previous variable phase's decisions: stop when every
+                // check is satisfied (oracle: after that iteration)
+                if (!__syncthreads_or(unsat | (it == 0))) break;
+            } else {
+                __syncthreads();
+            }
+            if (!MC && it == iters - 1) break;  // the last variable phase only forms posteriors
             // ---- variable phase ----
+            int errs = 0;
             if constexpr (LDPC_ABLATE_PHASE != 2) {
 #pragma unroll
                 for (int k = 0; k < KP; ++k) {
-                    var_pair(int_c<DVN0>{}, bool_c<ABS0>{}, 2 * k);
+                    const int d0 = var_pair(int_c<DVN0>{}, bool_c<ABS0>{}, 2 * k);
                     if (LDPC_LOC_VGROUP == 1) __builtin_amdgcn_sched_barrier(0);
-                    var_pair(int_c<DVN1>{}, bool_c<ABS1>{}, 2 * k + 1);
+                    const int d1 = var_pair(int_c<DVN1>{}, bool_c<ABS1>{}, 2 * k + 1);
                     if (LDPC_LOC_VGROUP > 0) __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (MC) errs += tid + k * T < a.loc_P ? __builtin_popcount(d0) + __builtin_popcount(d1) : 0;
                 }
             }
+            if constexpr (MC) {
+                const int w = wave_sum(errs);
+                if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[it + 1], w);
+            }
+        }
+        if constexpr (MC) {
+            __syncthreads();
+            int32_t *tr = a.trial + (size_t)b * (iters + 1);
+            const int last = curve[it];
+            for (int i = tid; i <= iters; i += T) tr[i] = i <= it ? curve[i] : last;
+            if (tid == 0) a.its[b] = it;
+            continue;
         }
         // ---- posteriors (after the last check phase) and outputs ----
         // (variable ids re-read where needed: not kept live through the decode loop)
@@ -3063,8 +3141,8 @@ bool loc_shape(const ldpc_graph &g, int &T, int &KP) {
     return (T == 256 && KP >= 1 && KP <= 4) || (T == 1024 && KP >= 2 && KP <= 3) ||
            (T == 512 && (KP == 8 || KP == 10) && rsu);
 }
-size_t loc_lds_bytes(const ldpc_graph &g) {
-    return ((size_t)std::max(g.loc_words + 64, g.n) * 4 + 15) & ~(size_t)15;
+size_t loc_lds_bytes(const ldpc_graph &g, int iters = 0, bool mc = false) {
+    return (((size_t)std::max(g.loc_words + 64, g.n) * 4 + 15) & ~(size_t)15) + (mc ? (size_t)(iters + 1) * 4 : 0);
 }
 
 // bp_irr_kernel: LDS bytes (messages, syndrome bits, curve) and whether the slab is used
@@ -3086,10 +3164,17 @@ size_t generic_lds_bytes(const ldpc_graph &g, int iters, bool mc) {
     return (((size_t)g.E * 5 + (size_t)g.n * 4 + 15) & ~(size_t)15) + (mc ? (size_t)(iters + 1) * 4 : 0);
 }
 
-BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc) {
+BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc, int algo = 0) {
     if (!g.consistent) return BpPath::None;
     int lT = 0, lKP = 0;
-    if (LDPC_LOC && !et && !mc && iters > 0 && loc_shape(g, lT, lKP) && loc_lds_bytes(g) <= kLdsMax - 2048)
+    // min-sum on the (3,6) code: bp_lds_kernel is faster (its variable sums need no
+    // reordering); the local-edge kernel for everything else it covers
+    // (Monte-Carlo with or without early stop: sum-product only; plain early-stop decodes,
+    // which return posteriors, stay on the other kernels)
+    const bool lds36_ms = algo == 1 && g.lane_var && g.dv == 3 && g.dc == 6;
+    const bool mode_ok = mc ? algo == 0 : !et;
+    if (LDPC_LOC && mode_ok && iters > 0 && !lds36_ms && loc_shape(g, lT, lKP) &&
+        loc_lds_bytes(g, iters, mc) <= kLdsMax - 2048)
         return BpPath::Loc;
     if (g.lane_var && g.dv == 3 && g.dc == 6 && lds36_bytes(g, iters, et, mc) <= kLdsMax - 2048)
         return BpPath::Lds36;
@@ -3159,34 +3244,30 @@ hipError_t launch_generic(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int DLO, int DHI, int D0, int D1, bool A0, bool A1, int T, int KP, int ALGO>
+template <int DLO, int DHI, int D0, int D1, bool A0, bool A1, int T, int KP, int ALGO, bool ET, bool MC>
 hipError_t launch_loc_shape(const ldpc_graph &g, const BpArgs &a, hipStream_t s) {
-    auto k = bp_loc_kernel<DLO, DHI, D0, D1, KP, T, ALGO, A0, A1>;
-    const size_t lds = loc_lds_bytes(g);
+    auto k = bp_loc_kernel<DLO, DHI, D0, D1, KP, T, ALGO, A0, A1, ET, MC>;
+    const size_t lds = loc_lds_bytes(g, a.max_iters, MC);
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(a.B), dim3(T), lds, s, a);
     return hipGetLastError();
 }
 
-template <int DLO, int DHI, int D0, int D1, bool A0, bool A1, int ALGO>
+template <int DLO, int DHI, int D0, int D1, bool A0, bool A1, int ALGO, bool ET, bool MC>
 hipError_t launch_loc_deg(const ldpc_graph &g, const BpArgs &a, int T, int KP, hipStream_t s) {
-    if (T == 256) {
-        if (KP == 1) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 256, 1, ALGO>(g, a, s);
-        if (KP == 2) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 256, 2, ALGO>(g, a, s);
-        if (KP == 3) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 256, 3, ALGO>(g, a, s);
-        if (KP == 4) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 256, 4, ALGO>(g, a, s);
-    } else if (T == 1024) {
-        if (KP == 2) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 1024, 2, ALGO>(g, a, s);
-        if (KP == 3) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 1024, 3, ALGO>(g, a, s);
-    } else if constexpr (DLO != DHI) {  // 512 threads, 2 waves per SIMD: the RSU-type shape only
-        if (KP == 8) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 512, 8, ALGO>(g, a, s);
-        if (KP == 10) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, 512, 10, ALGO>(g, a, s);
+#define LOC_SHAPE(TT, KK) \
+    if (T == TT && KP == KK) return launch_loc_shape<DLO, DHI, D0, D1, A0, A1, TT, KK, ALGO, ET, MC>(g, a, s);
+    LOC_SHAPE(256, 1) LOC_SHAPE(256, 2) LOC_SHAPE(256, 3) LOC_SHAPE(256, 4)
+    LOC_SHAPE(1024, 2) LOC_SHAPE(1024, 3)
+    if constexpr (DLO != DHI) {  // 512 threads, 2 waves per SIMD: the RSU-type shape only
+        LOC_SHAPE(512, 8) LOC_SHAPE(512, 10)
     }
+#undef LOC_SHAPE
     return hipErrorInvalidValue;
 }
 
-template <int ALGO>
+template <int ALGO, bool ET, bool MC>
 hipError_t launch_loc(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     int T = 0, KP = 0;
     if (!loc_shape(g, T, KP)) return hipErrorInvalidValue;
@@ -3201,8 +3282,8 @@ hipError_t launch_loc(const ldpc_graph &g, BpArgs a, hipStream_t s) {
         a.loc_cls_w[i] = g.loc_cls_w[i];
     }
     for (int i = 0; i < 4; ++i) a.loc_cls_d[i] = g.loc_cls_d[i];
-    if (g.loc_dlo == 6) return launch_loc_deg<6, 6, 2, 2, false, false, ALGO>(g, a, T, KP, s);
-    return launch_loc_deg<5, 6, 1, 3, false, true, ALGO>(g, a, T, KP, s);
+    if (g.loc_dlo == 6) return launch_loc_deg<6, 6, 2, 2, false, false, ALGO, ET, MC>(g, a, T, KP, s);
+    return launch_loc_deg<5, 6, 1, 3, false, true, ALGO, ET, MC>(g, a, T, KP, s);
 }
 
 template <int DC, int VPT, int ALGO, bool ET, bool MC>
@@ -3233,9 +3314,9 @@ hipError_t launch_irr(const ldpc_graph &g, BpArgs a, hipStream_t s) {
 
 template <int ALGO, bool ET, bool MC>
 hipError_t dispatch_bp(const ldpc_graph &g, BpArgs a, hipStream_t s) {
-    switch (choose_path(g, a.max_iters, ET, MC)) {
+    switch (choose_path(g, a.max_iters, ET, MC, ALGO)) {
         case BpPath::Loc:
-            if constexpr (!ET && !MC) return launch_loc<ALGO>(g, a, s);
+            if constexpr (MC ? ALGO == 0 : !ET) return launch_loc<ALGO, ET, MC>(g, a, s);
             return hipErrorInvalidValue;
         case BpPath::Lds36: return launch_lds36<ALGO, ET, MC>(g, a, s);
         case BpPath::Irr: return launch_irr<ALGO, ET, MC>(g, a, s);

@@ -313,3 +313,22 @@ def ref_bench_message_passing(words, iterations, check_lookup, variable_lookup, 
     used = lib_.ref_bench_message_passing(_p(w), B, iterations, _p(v2c), _p(c2v), _p(err), _p(its),
                                           n, k, dv, dc, int(threads))
     return w, err, its, used
+
+
+def ref_bench_timed(words, iterations, check_lookup, variable_lookup, n, k, dv, dc, threads, seconds):
+    """Time ref_bench_message_passing over chunks of `words` for ~`seconds` (call in a fresh
+    process: bench.py spawns one, so the OpenMP team is not confined by the parent's GPU /
+    torch runtime threads).  Returns (words decoded, elapsed s, OpenMP threads used)."""
+    import time
+    chunk = 64 * max(int(threads), 1)
+    done, i, used = 0, 0, 0
+    t0 = time.perf_counter()
+    while True:
+        lo = (i * chunk) % words.shape[0]
+        sl = words[lo:lo + chunk] if lo + chunk <= words.shape[0] else words[:chunk]
+        used = ref_bench_message_passing(sl, iterations, check_lookup, variable_lookup, n, k, dv, dc, threads)[3]
+        done += sl.shape[0]
+        i += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return done, el, used

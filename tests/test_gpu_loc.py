@@ -56,9 +56,10 @@ def test_loc_spa_vs_oracle(torch, monkeypatch, kind, n, noloc):
 
 @pytest.mark.parametrize("kind,n", CASES)
 def test_loc_minsum_bit_exact(torch, monkeypatch, kind, n):
+    """(min-sum on the (3,6) code dispatches to bp_lds_kernel, which is faster there; the
+    irregular cases exercise the local kernel's ordered variable sums)"""
     from iib_project_ldpc_codes_amd import decoder
     g, csr = _graph(kind, n, 22, False, monkeypatch)
-    assert g.kernel_name() == "bp_loc_kernel"
     llr = oracle.channel(oracle.CH_AWGN, 0.80, 6, 0, g.n, 32)
     post, hard, its = decoder.bp_decode(g, llr, 20, "minsum", alpha=0.75)
     opost, ohard, oits = oracle.bp_decode_batch(csr, llr, 20, 1, alpha=0.75)
@@ -80,3 +81,30 @@ def test_loc_spa_50_iterations(torch, monkeypatch, kind, n):
     assert same.mean() >= 0.99
     d = np.abs(post[same].astype(np.float64) - opost[same])
     assert np.mean(d <= 1e-3 + 1e-3 * np.abs(opost[same])) >= 0.999
+
+
+@pytest.mark.parametrize("kind,n,sigma", [("reg", 10000, 0.86), ("rsu", 20000, 0.84)])
+@pytest.mark.parametrize("early_stop", [True, False])
+def test_loc_mc_spa_vs_oracle(torch, monkeypatch, kind, n, sigma, early_stop):
+    """Fused Monte-Carlo sum-product on bp_loc_kernel (Philox channel, sign-bit syndrome early
+    stop): counters against the oracle's decodes of the same channel frames.  Sum-product is
+    compared to tolerance (the kernel's fp32 rule vs the oracle's exact one): frame errors
+    within 2, bit errors within 2 % + 20, iteration totals within 0.5 %."""
+    from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
+    g, csr = _graph(kind, n, 24, False, monkeypatch)
+    assert g.kernel_name() == "bp_loc_kernel"
+    B, iters = 128, 30
+    mc = MonteCarlo(g, "awgn", sigma, iters, algo="spa", early_stop=early_stop, seed=31, batch=B)
+    mc.run_batch(0, B)
+    torch.cuda.synchronize()
+    got = mc.counters.cpu().numpy()
+    llr = oracle.channel(oracle.CH_AWGN, sigma, 31, 0, g.n, B)
+    _, h, its = oracle.bp_decode_batch(csr, llr, iters, 0, early_stop=early_stop)
+    fe, be = int(h.any(axis=1).sum()), int(h.sum())
+    assert got[0] == B
+    assert 0 < fe < B  # both decoded and failed frames at this sigma
+    assert abs(int(got[1]) - fe) <= 2, (got[:4], fe, be, int(its.sum()))
+    assert abs(int(got[2]) - be) <= 0.02 * be + 20, (got[:4], fe, be)
+    assert abs(int(got[3]) - int(its.sum())) <= 0.005 * its.sum() + 2, (got[:4], int(its.sum()))
+    assert got[4] == int((llr < 0).sum())  # channel errors: bit-exact (Philox + fused channel)
+    assert got[4 + iters] == got[2]  # the last curve point is the final error count
