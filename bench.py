@@ -326,7 +326,7 @@ def main():
         # configs[3] shape: irregular RSU rate-1/2 ensemble (density-evolution lambda/rho),
         # n = 20000, BI-AWGN sum-product, 100 iterations, fixed count and with early stop
         from iib_project_ldpc_codes_amd import ensembles
-        gi = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1, deg2="zigzag")
+        gi = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1, deg2="path")  # ring code
         Bi = 8192
         llr_i = decoder.channel_dev("awgn", 0.80, 7, 0, gi.n, Bi)
         for key, et in (("irregular_cfg4_n20000_spa_100it", False), ("irregular_cfg4_n20000_spa_early_stop", True)):
@@ -340,6 +340,19 @@ def main():
                            "mean_iterations": float(its_i.float().mean().item()),
                            "kernel": gi.kernel_name(early_stop=et)}
         del llr_i
+        # configs[3] Monte-Carlo as scripts/fer_sweep.py runs it (fused channel, sign-bit early stop)
+        Bm = 65536
+        mc = MonteCarlo(gi, "awgn", 0.84, 100, algo="spa", early_stop=True, seed=9, batch=Bm)
+        mc.run_batch(0, Bm)
+        torch.cuda.synchronize()
+        a.record(stream)
+        mc.run_batch(Bm, Bm)
+        b.record(stream)
+        torch.cuda.synchronize()
+        cnt = mc.counters.cpu().numpy()
+        extras["irregular_cfg4_mc_sigma0.84_early_stop"] = {
+            "trials_per_s": Bm / (a.elapsed_time(b) * 1e-3), "batch": Bm, "mean_iterations": float(cnt[3] / cnt[0]),
+            "fer": float(cnt[1] / cnt[0])}
         # "optimal" modes: ML erasure decoding (parallel_simulator.py:60-129), n = 1000, eps = 0.45
         gm = TannerGraph.random_regular(1000, DV, DC, seed=1)
         wm = decoder.channel_dev("bec", 0.45, 5, 0, gm.n, 32768)

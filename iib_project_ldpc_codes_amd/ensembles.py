@@ -93,10 +93,18 @@ def sample_irregular(ens, n, seed=0, max_retries=100000, deg2="random", min_cycl
     deg2="zigzag": the degree-2 variables form a path through a random order of
     all checks (IRA-style) plus chords whose cycles through the path hold at
     least ``min_cycle`` degree-2 variables; the other variables are matched
-    uniformly to the remaining check sockets.  Same degree distributions, no
-    degree-2 codeword lighter than ``min_cycle``."""
-    if deg2 == "zigzag":
-        return _sample_zigzag(ens, n, seed, min_cycle, max_retries)
+    uniformly to the remaining check sockets.  Same degree distributions.  (The
+    chord test covers cycles through one or two chords only: cycles through three
+    or more chords, and codewords joining path segments through two degree-4
+    variables, remain -- they set its error floor, see DESIGN.md.)
+    deg2="path": a ring of m degree-2 variables through all checks and nothing
+    else: degree-2 variables beyond m become degree 3 (their extra sockets raise
+    the lowest check degrees, 5 -> 6), so the only all-degree-2 codeword is the
+    whole ring (weight m) and every lighter one needs variables of degree >= 3;
+    configs[3]'s code.  Each check then holds two degree-2 variables
+    (bp_loc_kernel's local slot 0)."""
+    if deg2 in ("zigzag", "path"):
+        return _sample_zigzag(ens, n, seed, min_cycle, max_retries, chords=deg2 == "zigzag")
     vdeg, cdeg = degree_sequences(ens, n)
     rng = np.random.default_rng(seed)
     E = int(vdeg.sum())
@@ -167,10 +175,16 @@ def _csr_from_pairs(n, m, cdeg, var_check_pairs):
     return TannerGraph.from_csr(cptr, cvar, vptr, vord.astype(np.int32))
 
 
-def _sample_zigzag(ens, n, seed, min_cycle, max_retries):
+def _sample_zigzag(ens, n, seed, min_cycle, max_retries, chords=True):
+    ring = not chords
     rng = np.random.default_rng(seed)
     vdeg, cdeg = degree_sequences(ens, n)
     m = cdeg.size
+    if ring:
+        extra = np.nonzero(vdeg == 2)[0][m:]  # the ring holds m of them
+        vdeg[extra] = 3
+        for _ in range(extra.size):  # one more socket on a lowest-degree check each
+            cdeg[int(np.argmin(cdeg))] += 1
     rng.shuffle(cdeg)
     d2 = np.nonzero(vdeg == 2)[0]
     others = np.nonzero(vdeg != 2)[0]
@@ -182,14 +196,16 @@ def _sample_zigzag(ens, n, seed, min_cycle, max_retries):
         pos[order] = np.arange(m)
         used = np.zeros(m, np.int64)
         pairs = []
-        for i in range(m - 1):                # the path: variable d2[i] on checks order[i], order[i+1]
-            a, b = order[i], order[i + 1]
+        for i in range(m if ring else m - 1):  # the path (ring): variable d2[i] on checks order[i], order[i+1]
+            a, b = order[i], order[(i + 1) % m]
             pairs += [(d2[i], a), (d2[i], b)]
             used[a] += 1
             used[b] += 1
+        if ring and d2.size != m:
+            raise ValueError("ring needs exactly m degree-2 variables")
         chords = []
         ok = True
-        for v in d2[m - 1:]:                  # chords between far-apart checks with spare sockets
+        for v in [] if ring else d2[m - 1:]:  # chords between far-apart checks with spare sockets
             for _try in range(1000):
                 a, b = rng.integers(0, m, 2)
                 if used[a] >= cdeg[a] or used[b] >= cdeg[b] or a == b:
@@ -224,6 +240,99 @@ def _sample_zigzag(ens, n, seed, min_cycle, max_retries):
                 break
         else:
             continue
+        if ring:
+            cs = _ring_repair(cs, vs, vdeg, pos, m, rng, min_cycle, max_retries)
+            if cs is None:
+                continue
         pairs += list(zip(vs.tolist(), cs.tolist()))
         return _csr_from_pairs(n, m, cdeg, pairs)
     raise RuntimeError("zigzag sampler: too many retries")
+
+
+def _ring_hops(cs, vs, vdeg, pos, m):
+    """Every pair of checks of one higher-degree variable ("hop") as ring positions:
+    arrays (socket_a, socket_b, variable, position_a, position_b)."""
+    sa, sb = [], []
+    start = 0
+    vdeg_s = vdeg[vs]
+    while start < vs.size:  # sockets are grouped by variable (np.repeat order)
+        d = int(vdeg_s[start])
+        stop = start
+        while stop < vs.size and vdeg_s[stop] == d:
+            stop += 1
+        base = np.arange(start, stop, d)
+        for i in range(d):
+            for j in range(i + 1, d):
+                sa.append(base + i)
+                sb.append(base + j)
+        start = stop
+    sa = np.concatenate(sa)
+    sb = np.concatenate(sb)
+    return sa, sb, vs[sa], pos[cs[sa]], pos[cs[sb]]
+
+
+def _ring_dist(x, y, m):
+    d = np.abs(x - y)
+    return np.minimum(d, m - d)
+
+
+def _ring_violations(cs, vs, vdeg, pos, m, min_cycle):
+    """Sockets to move so that no small trapping set is left through the ring:
+    (1) a higher-degree variable's checks >= min_cycle - 1 apart on the ring (a cycle
+    through it and the ring holds >= min_cycle variables; a degree-3 variable closing
+    a short ring segment is an (a, 1) trapping set); (2) two higher-degree variables
+    v, w joined by k ring segments of <= R = min_cycle // 4 degree-2 variables each
+    (distinct checks on both sides) with (deg v - k) + (deg w - k) <= 2 odd checks
+    left: two degree-3 variables twice joined, or two degree-4 ones thrice (the
+    theta-shaped (8, 2) sets of DESIGN.md's floor analysis)."""
+    sa, sb, hv, pa, pb = _ring_hops(cs, vs, vdeg, pos, m)
+    bad = set(sa[_ring_dist(pa, pb, m) < min_cycle - 1].tolist())
+    R = max(min_cycle // 4, 1)
+    p = pos[cs]
+    o = np.argsort(p, kind="stable")
+    pp = np.concatenate([p[o], p[o] + m])
+    oo = np.concatenate([o, o])
+    N = o.size
+    K = int((np.searchsorted(pp, pp[:N] + R, side="right") - np.arange(N)).max())
+    A, Bs = [], []
+    for k in range(1, K):
+        t = np.nonzero(pp[k:N + k] - pp[:N] <= R)[0]
+        A.append(oo[t])
+        Bs.append(oo[t + k])
+    s1 = np.concatenate(A)
+    s2 = np.concatenate(Bs)
+    v1, v2 = vs[s1], vs[s2]
+    keep = v1 != v2
+    s1, s2, v1, v2 = s1[keep], s2[keep], v1[keep], v2[keep]
+    sw = v1 > v2
+    s1, s2 = np.where(sw, s2, s1), np.where(sw, s1, s2)
+    v1, v2 = vs[s1], vs[s2]
+    n = int(vs.max()) + 1
+    pair = v1.astype(np.int64) * n + v2
+    if pair.size:
+        ka = np.unique(np.stack([pair, s1]), axis=1)[0]
+        kb = np.unique(np.stack([pair, s2]), axis=1)[0]
+        ua, ca = np.unique(ka, return_counts=True)
+        ub, cb = np.unique(kb, return_counts=True)
+        kk = np.minimum(ca, cb)  # ua == ub: the same pair keys
+        da, db = vdeg[ua // n], vdeg[ub % n]
+        hit = ua[(da - kk) + (db - kk) <= 2]
+        if hit.size:
+            first = np.unique(pair, return_index=True)
+            idx = first[1][np.searchsorted(first[0], hit)]
+            bad.update(s1[idx].tolist())
+    return np.array(sorted(bad), np.int64)
+
+
+def _ring_repair(cs, vs, vdeg, pos, m, rng, min_cycle, max_rounds):
+    """Swap the sockets of violating variables with random ones until no short cycle
+    through the ring remains (_ring_violations); None when it does not settle."""
+    cs = cs.copy()
+    for _ in range(min(max_rounds, 200)):
+        bad = _ring_violations(cs, vs, vdeg, pos, m, min_cycle)
+        if bad.size == 0:
+            return cs
+        tgt = rng.integers(0, cs.size, bad.size)
+        for a, b in zip(bad.tolist(), tgt.tolist()):
+            cs[a], cs[b] = cs[b], cs[a]
+    return None

@@ -4,7 +4,7 @@ sys.path.insert(0, os.getcwd())
 import torch
 from iib_project_ldpc_codes_amd import decoder, ensembles
 from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
-g = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1, deg2=os.environ.get("DEG2", "zigzag"))
+g = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1, deg2=os.environ.get("DEG2", "path"))
 s = torch.cuda.current_stream()
 for sigma in (0.85, 0.80):
     B = int(os.environ.get("B", "8192"))

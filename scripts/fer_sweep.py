@@ -1,9 +1,11 @@
 """FER / BER waterfall sweeps on the device Monte-Carlo engine (configs[2] and configs[3]).
 
   cfg3: (3,6) n=10000, BSC, normalized min-sum, crossover sweep, ~1M trials per point
-  cfg4: RSU rate-1/2 irregular (zigzag degree-2 placement), n=20000, BI-AWGN, SPA, 100 it
+  cfg4: RSU rate-1/2 irregular (ring degree-2 placement, ensembles.py deg2="path"), n=20000,
+        BI-AWGN, SPA, 100 it
 One process per GPU (torchrun); trials shard by index, counters all-reduced per round.
-Each point stops at 200 frame errors (parallel_simulator.py:198), --trials, or --seconds.
+Each point stops at --stop-errors frame errors (200, parallel_simulator.py:198), --trials,
+or --seconds.
 
   python scripts/fer_sweep.py cfg3 [--trials 1000000] [--seconds 60]
   torchrun --nproc-per-node 8 scripts/fer_sweep.py cfg4 --seconds 300
@@ -34,6 +36,8 @@ def main():
     ap.add_argument("--checkpoint-dir", type=str, default=None,
                     help="snapshot each point there every round; a rerun resumes from it (snapshot.py)")
     ap.add_argument("--seed", type=int, default=11)
+    ap.add_argument("--stop-errors", type=int, default=200)
+    ap.add_argument("--deg2", default="path", help="cfg4 degree-2 placement (ensembles.sample_irregular)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -47,7 +51,7 @@ def main():
         points = [float(p) for p in (args.points or "0.07,0.065,0.06,0.055,0.05").split(",")]
         batch = args.batch or 65536
     else:
-        g = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1, deg2="zigzag")
+        g = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1, deg2=args.deg2)
         channel, algo, alpha, iters = "awgn", "spa", 1.0, 100
         points = [float(p) for p in (args.points or "0.86,0.84,0.82,0.80,0.78").split(",")]
         batch = args.batch or 16384
@@ -63,11 +67,11 @@ def main():
         torch.cuda.synchronize()
         t0 = time.time()
         trials0 = int(mc.snapshot()["counters"][0])
-        res = mc.run(num_tests=args.trials, stop_frame_errors=200, time_limit=args.seconds, checkpoint=ck)
+        res = mc.run(num_tests=args.trials, stop_frame_errors=args.stop_errors, time_limit=args.seconds, checkpoint=ck)
         torch.cuda.synchronize()
         el = time.time() - t0
         if rank == 0:
-            out = {"config": args.config, "channel": channel, "param": p, "algo": algo, "iterations": iters,
+            out = {"config": args.config, "deg2": args.deg2 if args.config == "cfg4" else None, "channel": channel, "param": p, "algo": algo, "iterations": iters,
                    "n": g.n, "rate": rate, "gpus": world, "trials": res["num_tests"],
                    "frame_errors": res["frame_errors"], "fer": res["fer"], "ber": res["ber"],
                    "mean_iterations": res["iterations"] / max(res["num_tests"], 1),

@@ -3,7 +3,7 @@ import ctypes as ct, os, sys
 sys.path.insert(0, os.getcwd())
 import numpy as np, torch
 from iib_project_ldpc_codes_amd import decoder, ensembles
-g = ensembles.sample_irregular(ensembles.RSU_DL4, int(os.environ.get("N", "20000")), seed=1, deg2=os.environ.get("DEG2", "zigzag"))
+g = ensembles.sample_irregular(ensembles.RSU_DL4, int(os.environ.get("N", "20000")), seed=1, deg2=os.environ.get("DEG2", "path"))
 print("kernel", g.kernel_name(), "E", g.num_edges, flush=True)
 B = 8192; it = int(os.environ.get("ITERS", "20")); algo = int(os.environ.get("ALGO", "0"))
 llr = decoder.channel_dev("awgn", 0.8, 7, 0, g.n, B)

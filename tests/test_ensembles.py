@@ -69,6 +69,57 @@ def test_zigzag_construction_preserves_degrees_and_removes_weight2():
         pairs.add(p)
 
 
+def _ring_order(g):
+    """Check order along the degree-2 ring of a deg2="path" graph (asserts it is one cycle)."""
+    cptr, cvar, vptr, vslot = g.csr
+    slot_check = np.repeat(np.arange(g.m), np.diff(cptr))
+    vdeg = np.diff(vptr)
+    nb = [[] for _ in range(g.m)]
+    for v in np.nonzero(vdeg == 2)[0]:
+        a, b = slot_check[vslot[vptr[v]:vptr[v + 1]]]
+        nb[a].append(b)
+        nb[b].append(a)
+    assert all(len(x) == 2 for x in nb)  # every check on exactly two ring variables
+    order, prev, c = [0], -1, 0
+    while True:
+        nxt = nb[c][0] if nb[c][0] != prev else nb[c][1]
+        if nxt == 0:
+            break
+        order.append(nxt)
+        prev, c = c, nxt
+    assert len(order) == g.m  # one ring through all checks: the only all-degree-2 codeword
+    pos = np.empty(g.m, np.int64)
+    pos[order] = np.arange(g.m)
+    return pos, slot_check, vdeg
+
+
+def test_ring_construction_short_cycle_free():
+    """deg2="path": a ring of m degree-2 variables; no higher-degree variable closes a
+    ring segment shorter than min_cycle - 1, and no two degree-3 variables are joined by
+    two segments of <= min_cycle // 4 (the (a, 1) / (a, 2) trapping sets of the floor)."""
+    e, n, L = ensembles.RSU_DL4, 4000, 24
+    g = ensembles.sample_irregular(e, n, seed=2, deg2="path", min_cycle=L)
+    cptr, cvar, vptr, vslot = g.csr
+    assert np.array_equal(np.sort(vslot), np.arange(vslot.size))
+    vdeg0, cdeg0 = ensembles.degree_sequences(e, n)
+    assert cptr[-1] == vdeg0.sum() + np.count_nonzero(vdeg0 == 2) - g.m  # surplus degree 2 -> 3
+    pos, slot_check, vdeg = _ring_order(g)
+    m, R = g.m, L // 4
+    near = {}
+    for v in np.nonzero(vdeg > 2)[0]:
+        p = np.sort(pos[slot_check[vslot[vptr[v]:vptr[v + 1]]]])
+        d = np.diff(np.append(p, p[0] + m))
+        assert d.min() >= L - 1, (v, p)
+        if vdeg[v] == 3:
+            near[v] = p
+    items = list(near.items())
+    for i, (v, p) in enumerate(items):  # (3,3) pairs joined twice (brute force, n small)
+        for w, q in items[i + 1:]:
+            dd = np.abs(p[:, None] - q[None, :])
+            dd = np.minimum(dd, m - dd) <= R
+            assert not (dd.any(axis=1).sum() >= 2 and dd.any(axis=0).sum() >= 2), (v, w)
+
+
 def test_oracle_csr_sampler_regular_structure_equals_regular_sampler():
     """ldpc_sample_csr with v*dv / c*dc pointers is the regular generator."""
     from oracle import oracle

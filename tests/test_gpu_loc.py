@@ -2,9 +2,12 @@
 decodes with the layout disabled (LDPC_NO_LOC_LAYOUT=1 -> bp_lds_kernel / bp_irr_kernel /
 bp_generic_kernel) so both paths stay covered.  Shapes: (3,6) n = 1,000 (256 threads, one
 check pair each), n = 10,000 (the bench code: 1024 threads, 2-3 pairs), RSU rate-1/2
-irregular n = 2,000 and 20,000 (absent edges, two check-degree classes).  Tolerances as in
+irregular n = 2,000 and 20,000 (absent edges, two check-degree classes), with the zigzag
+and the ring (configs[3]'s code, ensembles.py deg2="path") degree-2 placements.  Tolerances as in
 test_gpu_parity.py: min-sum bit-exact; sum-product posteriors within SPA_* after 1-5
 iterations."""
+import functools
+
 import numpy as np
 import pytest
 
@@ -22,6 +25,12 @@ def torch():
     return t
 
 
+@functools.lru_cache(maxsize=None)
+def _rsu_csr(n, seed, deg2):
+    from iib_project_ldpc_codes_amd import ensembles
+    return tuple(np.asarray(a) for a in ensembles.sample_irregular(ensembles.RSU_DL4, n, seed=seed, deg2=deg2).to_csr())
+
+
 def _graph(kind, n, seed, noloc, monkeypatch):
     from iib_project_ldpc_codes_amd import ensembles
     from iib_project_ldpc_codes_amd.graph import TannerGraph
@@ -29,22 +38,22 @@ def _graph(kind, n, seed, noloc, monkeypatch):
         monkeypatch.setenv("LDPC_NO_LOC_LAYOUT", "1")
     else:
         monkeypatch.delenv("LDPC_NO_LOC_LAYOUT", raising=False)
-    if kind == "rsu":
-        g = ensembles.sample_irregular(ensembles.RSU_DL4, n, seed=seed, deg2="zigzag")
+    if kind in ("rsu", "ring"):
+        g = TannerGraph.from_csr(*_rsu_csr(n, seed, "zigzag" if kind == "rsu" else "path"))
     else:
         g = TannerGraph.random_regular(n, 3, 6, seed=seed)
     g.handle()  # the layout is built (or not) now, under this environment
     return g, [np.ascontiguousarray(a, np.int32) for a in g.to_csr()]
 
 
-CASES = [("reg", 1000), ("reg", 10000), ("rsu", 2000), ("rsu", 20000)]
+CASES = [("reg", 1000), ("reg", 10000), ("rsu", 2000), ("rsu", 20000), ("ring", 20000)]
 
 
 @pytest.mark.parametrize("kind,n", CASES)
 @pytest.mark.parametrize("noloc", [False, True])
 def test_loc_spa_vs_oracle(torch, monkeypatch, kind, n, noloc):
     from iib_project_ldpc_codes_amd import decoder
-    g, csr = _graph(kind, n, 21, noloc, monkeypatch)
+    g, csr = _graph(kind, n, 21 if kind != "ring" else 1, noloc, monkeypatch)
     assert (g.kernel_name() == "bp_loc_kernel") != noloc
     llr = oracle.channel(oracle.CH_AWGN, 0.82, 5, 0, g.n, 32)
     for iters in (1, 3, 5):
@@ -59,7 +68,7 @@ def test_loc_minsum_bit_exact(torch, monkeypatch, kind, n):
     """(min-sum on the (3,6) code dispatches to bp_lds_kernel, which is faster there; the
     irregular cases exercise the local kernel's ordered variable sums)"""
     from iib_project_ldpc_codes_amd import decoder
-    g, csr = _graph(kind, n, 22, False, monkeypatch)
+    g, csr = _graph(kind, n, 22 if kind != "ring" else 1, False, monkeypatch)
     llr = oracle.channel(oracle.CH_AWGN, 0.80, 6, 0, g.n, 32)
     post, hard, its = decoder.bp_decode(g, llr, 20, "minsum", alpha=0.75)
     opost, ohard, oits = oracle.bp_decode_batch(csr, llr, 20, 1, alpha=0.75)
@@ -83,7 +92,7 @@ def test_loc_spa_50_iterations(torch, monkeypatch, kind, n):
     assert np.mean(d <= 1e-3 + 1e-3 * np.abs(opost[same])) >= 0.999
 
 
-@pytest.mark.parametrize("kind,n,sigma", [("reg", 10000, 0.86), ("rsu", 20000, 0.84)])
+@pytest.mark.parametrize("kind,n,sigma", [("reg", 10000, 0.86), ("rsu", 20000, 0.84), ("ring", 20000, 0.88)])
 @pytest.mark.parametrize("early_stop", [True, False])
 def test_loc_mc_spa_vs_oracle(torch, monkeypatch, kind, n, sigma, early_stop):
     """Fused Monte-Carlo sum-product on bp_loc_kernel (Philox channel, sign-bit syndrome early
@@ -91,7 +100,7 @@ def test_loc_mc_spa_vs_oracle(torch, monkeypatch, kind, n, sigma, early_stop):
     compared to tolerance (the kernel's fp32 rule vs the oracle's exact one): frame errors
     within 2, bit errors within 2 % + 20, iteration totals within 0.5 %."""
     from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
-    g, csr = _graph(kind, n, 24, False, monkeypatch)
+    g, csr = _graph(kind, n, 24 if kind != "ring" else 1, False, monkeypatch)
     assert g.kernel_name() == "bp_loc_kernel"
     B, iters = 128, 30
     mc = MonteCarlo(g, "awgn", sigma, iters, algo="spa", early_stop=early_stop, seed=31, batch=B)
