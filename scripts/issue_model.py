@@ -1,18 +1,17 @@
 """Issue model of the headline decode kernel per codeword-iteration -> profiles/<tag>_issue_model.json.
 
-usage: python scripts/issue_model.py <kernels.s> <pmc_summary.json> <out.json> [git-sha]
+usage: python scripts/issue_model.py <kernels.s> <pmc_summary.json> <out.json> [git-sha] [--kernel loc|lds36]
 
 <kernels.s>: `hipcc --cuda-device-only -S` of csrc/ldpc_kernels.hip with the Makefile's flags;
 <pmc_summary.json>: scripts/pmc_summary.py output for one bench launch (B = 65,536, 50 iterations).
 
-The two on-chip units the LDS-resident kernel can saturate, per codeword-iteration of
-bp_lds_kernel<3,6,1024,10,SPA> (fixed count):
+The two on-chip units an LDS-resident decode kernel can saturate, per codeword-iteration:
 
 * VALU issue (per SIMD): wave-instructions by class x issue cycles of one wave64 instruction
   on its SIMD (MI355X_MICROARCH.md: v_fma_f32 2 cycles on the SIMD-32, packed f32 twice that,
-  transcendentals 8).  packed = the ISA's v_pk_* of the check and variable blocks x their
-  wave-executions; trans = PMC SQ_INSTS_VALU_TRANS_F32; plain = PMC SQ_INSTS_VALU - packed -
-  trans.  Peak: 1024 SIMDs.
+  transcendentals 8).  packed = the ISA's v_pk_* of every block x its wave-executions;
+  trans = PMC SQ_INSTS_VALU_TRANS_F32; plain = PMC SQ_INSTS_VALU - packed - trans.
+  Peak: 1024 SIMDs.
 * LDS (per CU): the blocks' ds_* wave-instructions x their conflict-free LDS cycles
   (MI355X_MICROARCH.md LDS table: ds_read_b128 4, ds_write_b128 13, ds_read_b32 2,
   ds_write_b32 4) -- the algorithmic LDS work.  PMC SQ_LDS_BANK_CONFLICT is reported beside it
@@ -20,53 +19,94 @@ bp_lds_kernel<3,6,1024,10,SPA> (fixed count):
   counter also tallies store conflicts that hide under a ds_write_b32's 4-cycle address +
   data transfer (2 LDS-array cycles).  Peak: 256 CUs.
 
-Wave-executions: the check phase's P = m/2 = 2500 pairs over T = 1024 threads (thread t owns
-pairs t, t+T, t+2T < P); the loop runs two pairs per iteration after a one-pair prologue for
-odd trip counts, so the prologue block runs in the waves holding a lane with 3 pairs (8) and
-the two-pair block once in every wave (16); the variable block runs once per wave (16).
+Wave-executions per codeword-iteration:
+
+--kernel loc (default; bp_loc_kernel<6,6,2,2,3,1024,SPA>, the bench code's local-edge
+  layout): the check phase is KP = 3 straight blocks (one per check pair slot k; each two
+  ds_read_b128 + two ds_write_b128 -- a pair's 2 x 4 non-local inputs and outputs), block k
+  runs in the waves holding a lane t with t + k*T < P (P = m/2 = 2500, T = 1024: 16, 16, 8
+  waves); the variable phase is one block (8*KP ds_read_b32 + 8*KP ds_write_b32: the 4*KP
+  local variables' 2 non-local edges each) run by all T/64 = 16 waves in ITERS - 1 of the
+  ITERS iterations (the last iteration's variable phase is the posterior epilogue); every
+  other block (staging, init, epilogue) counts once per wave per codeword, i.e. 16/ITERS.
+--kernel lds36 (round-2 bp_lds_kernel<3,6,1024,10,SPA>): the check phase's two-pair loop body
+  (16 wave-executions) after a one-pair prologue (8), the variable block once per wave (16).
 """
 import collections
 import json
 import sys
 
 sys.path.insert(0, __file__.rsplit("/", 1)[0])
-from valu_mix import KERNEL, blocks, mix  # noqa: E402
+from valu_mix import blocks, mix  # noqa: E402
 
-N, DV, DC, T, B, ITERS = 10000, 3, 6, 1024, 65536, 50
+N, DV, DC, B, ITERS = 10000, 3, 6, 65536, 50
 LDS_CYC = {"ds_read_b128": 4, "ds_write_b128": 13, "ds_read_b32": 2, "ds_write_b32": 4,
-           "ds_read_b64": 2, "ds_write_b64": 6}
+           "ds_read_b64": 2, "ds_write_b64": 6, "ds_write2st64_b32": 8, "ds_write2_b32": 8,
+           "ds_read2_b32": 4, "ds_read2st64_b32": 4}
 VALU_CYC = {"packed": 4.0, "plain": 2.0, "trans": 8.0}
+KERNELS = {
+    "loc": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi3ELi1024ELi0ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
+            "bp_loc_kernel<6,6,2,2,KP=3,T=1024,SPA,fixed-count>", 1024, 3),
+    "lds36": ("_ZN4ldpc12_GLOBAL__N_113bp_lds_kernelILi3ELi6ELi1024ELi10ELi0ELb0ELb0EEEvNS0_6BpArgsE",
+              "bp_lds_kernel<3,6,1024,10,SPA,fixed-count>", 1024, None),
+}
 
 
-def wave_execs():
+def loc_parts(bb, T, KP):
     P = (N * DV // DC) // 2
-    trips = [len(range(t, P, T)) for t in range(T)]
-    pro = sum(1 for w in range(T // 64) if any(trips[t] % 2 for t in range(64 * w, 64 * w + 64)))
-    two = sum(max(trips[t] // 2 for t in range(64 * w, 64 * w + 64)) for w in range(T // 64))
-    return pro, two, T // 64
+    waves = T // 64
+    chk = [i for i, (_, ins) in enumerate(bb) if ins.count("ds_read_b128") == 2 and ins.count("ds_write_b128") == 2]
+    assert len(chk) == KP, len(chk)
+    var = max(range(len(bb)), key=lambda i: bb[i][1].count("ds_read_b32"))
+    assert bb[var][1].count("ds_read_b32") == 8 * KP and bb[var][1].count("ds_write_b32") == 8 * KP
+    execs = {}
+    for k, i in enumerate(chk):
+        lanes = min(max(P - k * T, 0), T)
+        execs[i] = (lanes + 63) // 64
+    execs[var] = waves * (ITERS - 1) / ITERS
+    parts = []
+    for i, (_, ins) in enumerate(bb):
+        parts.append((ins, execs.get(i, waves / ITERS)))
+    return parts, {"check_slot_waves": [execs[i] for i in chk], "variable": execs[var],
+                   "other_blocks": waves / ITERS}
 
 
-def main():
-    src, pmc_path, out_path = sys.argv[1:4]
-    sha = sys.argv[4] if len(sys.argv) > 4 else None
-    lines = open(src).read().split("\n")
-    a = next(k for k, l in enumerate(lines) if l.startswith(KERNEL + ":"))
-    b = next(k for k in range(a, len(lines)) if "s_endpgm" in lines[k])
-    bb = blocks(lines[a:b])
+def lds36_parts(bb, T):
     one = [ins for _, ins in bb if ins.count("ds_read_b128") == 3]
     two = [ins for _, ins in bb if ins.count("ds_read_b128") == 6]
     var = max((ins for _, ins in bb), key=lambda ins: ins.count("ds_read_b32"))
     assert len(one) == 1 and len(two) == 1 and var.count("ds_read_b32") == 3 * 10
-    n_one, n_two, n_var = wave_execs()
+    P = (N * DV // DC) // 2
+    trips = [len(range(t, P, T)) for t in range(T)]
+    n_one = sum(1 for w in range(T // 64) if any(trips[t] % 2 for t in range(64 * w, 64 * w + 64)))
+    n_two = sum(max(trips[t] // 2 for t in range(64 * w, 64 * w + 64)) for w in range(T // 64))
     assert n_one + 2 * n_two == 40
-    parts = [(one[0], n_one), (two[0], n_two), (var, n_var)]
+    return [(one[0], n_one), (two[0], n_two), (var, T // 64)], \
+        {"check_one_pair": n_one, "check_two_pairs": n_two, "variable": T // 64}
+
+
+def main():
+    argv = [a for a in sys.argv[1:] if not a.startswith("--")]
+    kind = "loc"
+    if "--kernel" in sys.argv:
+        kind = sys.argv[sys.argv.index("--kernel") + 1]
+        argv.remove(kind)
+    src, pmc_path, out_path = argv[:3]
+    sha = argv[3] if len(argv) > 3 else None
+    sym, label, T, KP = KERNELS[kind]
+    lines = open(src).read().split("\n")
+    a = next(k for k, l in enumerate(lines) if l.startswith(sym + ":"))
+    b = next(k for k in range(a, len(lines)) if "s_endpgm" in lines[k])
+    bb = blocks(lines[a:b])
+    parts, wx = loc_parts(bb, T, KP) if kind == "loc" else lds36_parts(bb, T)
     valu = collections.Counter()
     lds = collections.Counter()
     for ins, k in parts:
         for c, v in mix(ins).items():
             valu[c] += v * k
         for op in ins:
-            if op in LDS_CYC:
+            if op.startswith("ds_"):
+                assert op in LDS_CYC, op
                 lds[op] += k
     d = json.load(open(pmc_path))["counters"]
     units = B * ITERS
@@ -76,7 +116,8 @@ def main():
     conflict = d["SQ_LDS_BANK_CONFLICT"] / units
     lds_cycles = sum(LDS_CYC[op] * n for op, n in lds.items())
     out = {
-        "kernel": "bp_lds_kernel<3,6,1024,10,SPA,fixed-count>",
+        "kernel": label,
+        "kernel_family": label.split("<")[0],
         "git": sha,
         "wave_instr_per_codeword_iteration": per,
         "valu_issue_cycles_per_codeword_iteration": sum(per[c] * VALU_CYC[c] for c in VALU_CYC),
@@ -85,12 +126,13 @@ def main():
         "lds_cycles_per_codeword_iteration": lds_cycles,
         "cycles": {"valu": VALU_CYC, "lds": LDS_CYC},
         "check": {"isa_valu_per_codeword_iteration": valu["packed"] + valu["plain"] + valu["trans"],
+                  "isa_trans_per_codeword_iteration": valu["trans"],
                   "pmc_valu_per_codeword_iteration": total,
                   "isa_lds_per_codeword_iteration": sum(lds.values()),
                   "pmc_lds_per_codeword_iteration": d.get("SQ_INSTS_LDS", 0) / units,
                   "isa_pk_mul_fma": valu["pk_mul_fma"],
                   "pmc_mul_fma_f32": (d.get("SQ_INSTS_VALU_MUL_F32", 0) + d.get("SQ_INSTS_VALU_FMA_F32", 0)) / units},
-        "wave_executions": {"check_one_pair": n_one, "check_two_pairs": n_two, "variable": n_var},
+        "wave_executions": wx,
         "pmc_per_codeword_iteration": {k: v / units for k, v in d.items() if k.startswith("SQ_")},
     }
     json.dump(out, open(out_path, "w"), indent=1)
