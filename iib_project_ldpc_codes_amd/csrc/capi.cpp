@@ -408,11 +408,22 @@ int device_graph(const HostGraph &h, ldpc_graph **out) {
     const char *noloc = getenv("LDPC_NO_LOC_LAYOUT");
     if (e == hipSuccess && h.consistent && LDPC_LOC_LAYOUT && !(noloc && noloc[0] == '1')) {
         LocLayout L;
-        // threads: 256 for up to 1024 check pairs (4 per thread), 1024 for up to 3072 (3 per
-        // thread: 4 do not fit 128 VGPRs), else 512 threads with 256 VGPRs (up to 10 per thread)
+        // threads: 256 for up to 1024 check pairs (4 per thread); (3,6) codes up to 2560 pairs:
+        // 512 threads x 5 pairs, two workgroups per CU when both fit the LDS (the bench code:
+        // +29 % over one 1024-thread workgroup, whose barriers idle the CU); 1024 for up to
+        // 3072 (3 per thread: 4 do not fit 128 VGPRs), else 512 threads with 256 VGPRs (up to
+        // 10 per thread)
         const int P = h.m / 2;
-        L.T = P <= 1024 ? 256 : (P <= 3072 ? 1024 : 512);
-        if (build_loc_layout(h.n, h.m, h.cptr, h.cvar, h.vptr, h.vslot, L)) {
+        const bool r36 = h.dv == 3 && h.dc == 6;
+        L.T = P <= 1024 ? 256 : (r36 && P <= 2560 ? 512 : (P <= 3072 ? 1024 : 512));
+        if (const char *t = getenv("LDPC_LOC_T")) L.T = atoi(t);  // shape experiments
+        bool built = build_loc_layout(h.n, h.m, h.cptr, h.cvar, h.vptr, h.vslot, L);
+        if (built && r36 && L.T == 512 && L.KP == 5 && (size_t)std::max(L.words + 64, h.n) * 4 > 80 * 1024) {
+            L = LocLayout();  // two workgroups would not fit one CU's LDS
+            L.T = 1024;
+            built = build_loc_layout(h.n, h.m, h.cptr, h.cvar, h.vptr, h.vslot, L);
+        }
+        if (built) {
             e = upload(&g->loc_var, L.var);
             if (e == hipSuccess) e = upload(&g->loc_pos, L.pos);
             if (e == hipSuccess) e = upload(&g->loc_info, L.info);

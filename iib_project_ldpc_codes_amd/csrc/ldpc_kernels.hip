@@ -52,6 +52,9 @@ constexpr int kWave = 64;
 #ifndef LDPC_LOC_VGROUP
 #define LDPC_LOC_VGROUP 1  // bp_loc_kernel: variable pairs per scheduling group (0: no barriers)
 #endif
+#ifndef LDPC_LOC_LAUNDER_SP
+#define LDPC_LOC_LAUNDER_SP 1  // bp_loc_kernel: no loop-invariant unpacked gather addresses
+#endif
 #ifndef LDPC_LOC_CGROUP
 #define LDPC_LOC_CGROUP 1  // bp_loc_kernel: check pairs per scheduling group (0: no barriers)
 #endif
@@ -1523,9 +1526,13 @@ template <bool B> using bool_c = std::integral_constant<bool, B>;
 // MC (sum-product): fused Philox channel, per-iteration error counts of the all-zero
 // codeword into the trial curve, no posteriors; ET with MC: syndrome early stop on the
 // sign-bit decisions (see loc_check_pair).
+// 512 threads with up to 5 check pairs each: two workgroups per CU (4 waves per SIMD, <= 128
+// VGPRs), so one workgroup's barrier waits overlap the other's work; else one workgroup
+constexpr int loc_waves_per_simd(int T, int KP) { return T == 512 && KP <= 5 ? 4 : 1; }
+
 template <int DLO, int DHI, int DVN0, int DVN1, int KP, int T, int ALGO, bool ABS0, bool ABS1, bool ET = false,
           bool MC = false>
-__global__ __launch_bounds__(T) void bp_loc_kernel(BpArgs a) {
+__global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(BpArgs a) {
     static_assert(!ET || (MC && ALGO == 0), "early stop: sum-product Monte-Carlo only");
     constexpr int VP = 2 * KP;  // variable pairs per thread
     constexpr int DVM = DVN0 > DVN1 ? DVN0 : DVN1;
@@ -1701,6 +1708,12 @@ __global__ __launch_bounds__(T) void bp_loc_kernel(BpArgs a) {
         for (; it < iters; ++it) {
             __syncthreads();  // variable phase (or initialisation) complete
             int unsat = 0;
+            if constexpr (LDPC_LOC_LAUNDER_SP) {  // the gathers' unpacked addresses stay in the loop
+#pragma unroll
+                for (int v = 0; v < VP; ++v)
+#pragma unroll
+                    for (int u = 0; u < DVA; ++u) asm volatile("" : "+v"(sp[v][u]));
+            }
             // ---- check phase ----
 #pragma unroll
             for (int k = 0; k < KP; ++k) {
@@ -3123,6 +3136,9 @@ BecArgs bec_args(const ldpc_graph &g) {
 // --- soft path selection ---------------------------------------------------
 enum class BpPath { Loc, Lds36, Irr, Generic8, Generic16, Generic32, GenericG8, GenericG16, GenericG32, None };
 
+#ifndef LDPC_LDS36_MINSUM
+#define LDPC_LDS36_MINSUM 1  // (3,6) min-sum on bp_lds_kernel rather than bp_loc_kernel
+#endif
 #ifndef LDPC_LOC
 #define LDPC_LOC 1  // fixed-count decode on bp_loc_kernel when the graph has a local-edge layout
 #endif
@@ -3139,7 +3155,7 @@ bool loc_shape(const ldpc_graph &g, int &T, int &KP) {
     T = g.loc_T;
     KP = g.loc_KP;
     return (T == 256 && KP >= 1 && KP <= 4) || (T == 1024 && KP >= 2 && KP <= 3) ||
-           (T == 512 && (KP == 8 || KP == 10) && rsu);
+           (T == 512 && (KP == 8 || KP == 10) && rsu) || (T == 512 && KP == 5 && reg36);
 }
 size_t loc_lds_bytes(const ldpc_graph &g, int iters = 0, bool mc = false) {
     return (((size_t)std::max(g.loc_words + 64, g.n) * 4 + 15) & ~(size_t)15) + (mc ? (size_t)(iters + 1) * 4 : 0);
@@ -3167,11 +3183,13 @@ size_t generic_lds_bytes(const ldpc_graph &g, int iters, bool mc) {
 BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc, int algo = 0) {
     if (!g.consistent) return BpPath::None;
     int lT = 0, lKP = 0;
-    // min-sum on the (3,6) code: bp_lds_kernel is faster (its variable sums need no
-    // reordering); the local-edge kernel for everything else it covers
+    // min-sum on (3,6) codes with one 1024-thread local-edge workgroup per CU: bp_lds_kernel
+    // is faster (its variable sums need no reordering); with the two-workgroup 512-thread
+    // shape the local-edge kernel wins (bench code: 2.00 vs 1.74 M cw/s); the local-edge
+    // kernel for everything else it covers
     // (Monte-Carlo with or without early stop: sum-product only; plain early-stop decodes,
     // which return posteriors, stay on the other kernels)
-    const bool lds36_ms = algo == 1 && g.lane_var && g.dv == 3 && g.dc == 6;
+    const bool lds36_ms = LDPC_LDS36_MINSUM && algo == 1 && g.lane_var && g.dv == 3 && g.dc == 6 && g.loc_T != 512;
     const bool mode_ok = mc ? algo == 0 : !et;
     if (LDPC_LOC && mode_ok && iters > 0 && !lds36_ms && loc_shape(g, lT, lKP) &&
         loc_lds_bytes(g, iters, mc) <= kLdsMax - 2048)
@@ -3262,6 +3280,8 @@ hipError_t launch_loc_deg(const ldpc_graph &g, const BpArgs &a, int T, int KP, h
     LOC_SHAPE(1024, 2) LOC_SHAPE(1024, 3)
     if constexpr (DLO != DHI) {  // 512 threads, 2 waves per SIMD: the RSU-type shape only
         LOC_SHAPE(512, 8) LOC_SHAPE(512, 10)
+    } else {  // 512 threads, two workgroups per CU
+        LOC_SHAPE(512, 5)
     }
 #undef LOC_SHAPE
     return hipErrorInvalidValue;

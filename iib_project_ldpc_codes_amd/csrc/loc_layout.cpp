@@ -229,7 +229,7 @@ bool build_loc_layout(int n, int m, const std::vector<int32_t> &cptr, const std:
         else L.ABS1 |= nd != L.DVN1;
     }
     L.KP = (L.P + L.T - 1) / L.T;
-    if (L.T == 512) L.KP = L.KP <= 8 ? 8 : 10;  // the instantiated 512-thread shapes
+    if (L.T == 512) L.KP = L.KP <= 5 ? 5 : (L.KP <= 8 ? 8 : 10);  // the instantiated 512-thread shapes
     if ((long)L.KP * L.T < L.P || L.words + 64 >= 65536) return false;  // beyond 16-bit words / the shapes
     // Bank-conflict search.  A variable's non-local edge u is gathered (and written) by
     // one instruction (var pair slot, u, half) of its thread; the 32 lanes of a half wave

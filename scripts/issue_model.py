@@ -21,14 +21,16 @@ The two on-chip units an LDS-resident decode kernel can saturate, per codeword-i
 
 Wave-executions per codeword-iteration:
 
---kernel loc (default; bp_loc_kernel<6,6,2,2,3,1024,SPA>, the bench code's local-edge
-  layout): the check phase is KP = 3 straight blocks (one per check pair slot k; each two
-  ds_read_b128 + two ds_write_b128 -- a pair's 2 x 4 non-local inputs and outputs), block k
-  runs in the waves holding a lane t with t + k*T < P (P = m/2 = 2500, T = 1024: 16, 16, 8
-  waves); the variable phase is one block (8*KP ds_read_b32 + 8*KP ds_write_b32: the 4*KP
-  local variables' 2 non-local edges each) run by all T/64 = 16 waves in ITERS - 1 of the
-  ITERS iterations (the last iteration's variable phase is the posterior epilogue); every
-  other block (staging, init, epilogue) counts once per wave per codeword, i.e. 16/ITERS.
+--kernel loc (default; bp_loc_kernel<6,6,2,2,5,512,SPA>, the bench code's local-edge
+  layout, two 512-thread workgroups per CU): the check phase is KP = 5 straight blocks (one
+  per check pair slot k; each two ds_read_b128 + two ds_write_b128 -- a pair's 2 x 4
+  non-local inputs and outputs), block k runs in the waves holding a lane t with
+  t + k*T < P (P = m/2 = 2500, T = 512: 8 waves each); the variable phase is one block
+  (8*KP ds_read_b32 + 8*KP ds_write_b32: the 4*KP local variables' 2 non-local edges each)
+  run by all T/64 = 8 waves in ITERS - 1 of the ITERS iterations (the last iteration's
+  variable phase is the posterior epilogue); every other block (staging, init, epilogue)
+  counts once per wave per codeword, i.e. 8/ITERS.  --kernel loc1024: the round-2
+  one-workgroup shape <6,6,2,2,3,1024> (16, 16, 8 waves; 16).
 --kernel lds36 (round-2 bp_lds_kernel<3,6,1024,10,SPA>): the check phase's two-pair loop body
   (16 wave-executions) after a one-pair prologue (8), the variable block once per wave (16).
 """
@@ -45,8 +47,10 @@ LDS_CYC = {"ds_read_b128": 4, "ds_write_b128": 13, "ds_read_b32": 2, "ds_write_b
            "ds_read2_b32": 4, "ds_read2st64_b32": 4}
 VALU_CYC = {"packed": 4.0, "plain": 2.0, "trans": 8.0}
 KERNELS = {
-    "loc": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi3ELi1024ELi0ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
-            "bp_loc_kernel<6,6,2,2,KP=3,T=1024,SPA,fixed-count>", 1024, 3),
+    "loc": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi5ELi512ELi0ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
+            "bp_loc_kernel<6,6,2,2,KP=5,T=512,SPA,fixed-count>", 512, 5),
+    "loc1024": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi3ELi1024ELi0ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
+                "bp_loc_kernel<6,6,2,2,KP=3,T=1024,SPA,fixed-count>", 1024, 3),
     "lds36": ("_ZN4ldpc12_GLOBAL__N_113bp_lds_kernelILi3ELi6ELi1024ELi10ELi0ELb0ELb0EEEvNS0_6BpArgsE",
               "bp_lds_kernel<3,6,1024,10,SPA,fixed-count>", 1024, None),
 }
@@ -98,7 +102,7 @@ def main():
     a = next(k for k, l in enumerate(lines) if l.startswith(sym + ":"))
     b = next(k for k in range(a, len(lines)) if "s_endpgm" in lines[k])
     bb = blocks(lines[a:b])
-    parts, wx = loc_parts(bb, T, KP) if kind == "loc" else lds36_parts(bb, T)
+    parts, wx = loc_parts(bb, T, KP) if kind.startswith("loc") else lds36_parts(bb, T)
     valu = collections.Counter()
     lds = collections.Counter()
     for ins, k in parts:

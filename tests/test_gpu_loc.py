@@ -65,8 +65,8 @@ def test_loc_spa_vs_oracle(torch, monkeypatch, kind, n, noloc):
 
 @pytest.mark.parametrize("kind,n", CASES)
 def test_loc_minsum_bit_exact(torch, monkeypatch, kind, n):
-    """(min-sum on the (3,6) code dispatches to bp_lds_kernel, which is faster there; the
-    irregular cases exercise the local kernel's ordered variable sums)"""
+    """Min-sum through the local kernel's ordered variable sums (the (3,6) n = 1,000 code:
+    256-thread shape; n = 10,000: the two-workgroup 512-thread shape) -- bit-exact."""
     from iib_project_ldpc_codes_amd import decoder
     g, csr = _graph(kind, n, 22 if kind != "ring" else 1, False, monkeypatch)
     llr = oracle.channel(oracle.CH_AWGN, 0.80, 6, 0, g.n, 32)
