@@ -1548,28 +1548,29 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     constexpr bool INF0 = ABS0 || ALGO == 1, INF1 = ABS1 || ALGO == 1;
     uint32_t sp[VP][DVA];
     uint32_t inf[VP];
-    auto dvn_of = [](auto s_tag) { return decltype(s_tag)::value ? DVN1 : DVN0; };
+    // packed LDS word pair of var pair v's non-local edge u (re-read per codeword and for
+    // the posterior gathers: not held live outside the iteration loop, where the
+    // staging and epilogue need the VGPRs)
+    auto load_sp = [&](int v, int u) {
+        return (uint32_t)ld_fresh(a.loc_pos, (v * DVP + u) * T + tid) + base2;
+    };
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
-#pragma unroll
-        for (int u = 0; u < DVN0; ++u) sp[2 * k][u] = (uint32_t)a.loc_pos[((2 * k) * DVP + u) * T + tid] + base2;
-#pragma unroll
-        for (int u = 0; u < DVN1; ++u) sp[2 * k + 1][u] = (uint32_t)a.loc_pos[((2 * k + 1) * DVP + u) * T + tid] + base2;
         if constexpr (INF0) inf[2 * k] = (uint32_t)a.loc_info[(2 * k) * T + tid];
         if constexpr (INF1) inf[2 * k + 1] = (uint32_t)a.loc_info[(2 * k + 1) * T + tid];
     }
-    (void)dvn_of;
     auto at = [](uint32_t ba) -> lds_f32 & { return *(lds_f32 *)(size_t)ba; };
     const float neutral = SPA ? 1.0f : 0.0f;
 
     // gather the non-local c->v messages of var pair v (slot s) into cv[0 .. DN-1]
-    auto gather = [&](auto dn_tag, auto abs_tag, int v, float2 (&cv)[DVA], uint32_t (&a0)[DVA], uint32_t (&a1)[DVA]) {
+    auto gather = [&](auto dn_tag, auto abs_tag, int v, const uint32_t (&spv)[DVA], float2 (&cv)[DVA],
+                      uint32_t (&a0)[DVA], uint32_t (&a1)[DVA]) {
         constexpr int DN = decltype(dn_tag)::value;
         constexpr bool AB = decltype(abs_tag)::value;
 #pragma unroll
         for (int u = 0; u < DN; ++u) {
-            a0[u] = pos_lo_x4(sp[v][u]);
-            a1[u] = pos_hi_x4(sp[v][u]);
+            a0[u] = pos_lo_x4(spv[u]);
+            a1[u] = pos_hi_x4(spv[u]);
         }
 #pragma unroll
         for (int u = 0; u < DN; ++u) cv[u] = make_float2(at(a0[u]), at(a1[u]));
@@ -1623,6 +1624,13 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             const int w = wave_sum(err0);
             if ((tid & (kWave - 1)) == 0) atomicAdd(&curve[0], w);
         }
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+#pragma unroll
+            for (int u = 0; u < DVN0; ++u) sp[2 * k][u] = load_sp(2 * k, u);
+#pragma unroll
+            for (int u = 0; u < DVN1; ++u) sp[2 * k + 1][u] = load_sp(2 * k + 1, u);
+        }
         float2 L[VP];  // SPA: E = 2^channel (clamped); min-sum: channel LLR
 #pragma unroll
         for (int v = 0; v < VP; ++v) {
@@ -1661,7 +1669,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             constexpr int DV = DN + 1;
             uint32_t a0[DVA], a1[DVA];
             float2 cv[DVA];
-            gather(dn_tag, abs_tag, v, cv, a0, a1);
+            gather(dn_tag, abs_tag, v, sp[v], cv, a0, a1);
             int dec = 0;
             if constexpr (SPA) {
                 // edges e_0 = local, e_{1+u} = non-local u: R_j = E prod_{k != j} e_k
@@ -1780,9 +1788,11 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
         float2 pr[VP];
         auto post = [&](auto dn_tag, auto abs_tag, int v) {
             constexpr int DN = decltype(dn_tag)::value;
-            uint32_t a0[DVA], a1[DVA];
+            uint32_t a0[DVA], a1[DVA], spv[DVA];
             float2 cv[DVA];
-            gather(dn_tag, abs_tag, v, cv, a0, a1);
+#pragma unroll
+            for (int u = 0; u < DN; ++u) spv[u] = load_sp(v, u);
+            gather(dn_tag, abs_tag, v, spv, cv, a0, a1);
             if constexpr (SPA) {
                 const float *lb = a.llr + (size_t)b * n;
                 const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid), v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
