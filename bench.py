@@ -13,7 +13,7 @@ Weak scaling: every rank decodes its own 65536-frame batch.
 Rank 0 prints one JSON line.  roofline: the decode kernel keeps every edge
 message in LDS, so its binding unit is on-chip: LDS cycles (per CU) or VALU
 issue cycles (per SIMD) per codeword-iteration from the committed HEAD issue
-model (profiles/r02b_issue_model.json, scripts/issue_model.py) x the live
+model (profiles/r02c_issue_model.json, scripts/issue_model.py) x the live
 codeword-iteration rate of the kernel (HIP events on the launch stream) over
 the unit's peak; the larger fraction is `roofline`.  roofline.hbm_model
 keeps SURVEY.md 8(d)'s streaming byte model (2*E*4 + 2*n*4 = 320,000 B per
@@ -162,24 +162,27 @@ def graph_cfg0():
     return TannerGraph.random_regular(1000, DV, DC, seed=1)
 
 
-ISSUE_PROFILE = os.path.join(ROOT, "profiles", "r02b_issue_model.json")
+ISSUE_PROFILE = os.path.join(ROOT, "profiles", "r02c_issue_model.json")
 SIMDS, CUS, CLOCK_HZ = 1024, 256, 2.4e9
 
 
-def onchip_rooflines(cw_iters_per_s):
+def onchip_rooflines(cw_iters_per_s, kernel):
     """The units the LDS-resident kernel can saturate, from the committed HEAD issue model
-    (profiles/r02b_issue_model.json, scripts/issue_model.py: the kernel ISA's blocks x their
+    (profiles/r02c_issue_model.json, scripts/issue_model.py: the kernel ISA's blocks x their
     execution counts, cross-checked with and completed by the PMC counters of one launch):
       valu: issue cycles per codeword-iteration (packed f32 4, plain 2, transcendental 8 per
             wave64 instruction, MI355X_MICROARCH.md) over 1024 SIMDs x 2.4 GHz;
       lds:  LDS cycles per codeword-iteration (conflict-free per-instruction costs of the
             MI355X_MICROARCH.md LDS table; the measured bank-conflict cycles are reported
             beside it as waste) over 256 CUs x 2.4 GHz.
-    achieved = cycles x the live codeword-iteration rate of the kernel.  Returns (valu, lds)."""
+    achieved = cycles x the live codeword-iteration rate of the kernel.  Returns (valu, lds), or
+    (None, None) when the committed model is of another kernel than the one that ran."""
     if not os.path.exists(ISSUE_PROFILE):
         return None, None
     with open(ISSUE_PROFILE) as f:
         d = json.load(f)
+    if d.get("kernel_family") != kernel.split("<")[0]:  # the model describes another kernel: no roofline from it
+        return None, None
     rel = os.path.relpath(ISSUE_PROFILE, ROOT)
     v_cyc = d["valu_issue_cycles_per_codeword_iteration"]
     l_cyc = d["lds_cycles_per_codeword_iteration"]
@@ -198,7 +201,7 @@ def onchip_rooflines(cw_iters_per_s):
 
 
 def load_traffic():
-    for name in ("r02b_pmc_traffic.json", "r02_pmc_traffic.json", "pmc_traffic.json"):
+    for name in ("r02c_pmc_traffic.json", "r02b_pmc_traffic.json", "pmc_traffic.json"):
         p = os.path.join(ROOT, "profiles", name)
         if os.path.exists(p):
             with open(p) as f:
@@ -380,7 +383,7 @@ def main():
         hbm_model["measured_frac"] = hbm_meas / HBM_PEAK_GBPS
         hbm_model["measured_bytes_per_codeword"] = traffic["bytes_per_codeword"]
         hbm_model["traffic_profile"] = traffic.get("source", "profiles/pmc_traffic.json")
-    valu_roof, lds_roof = onchip_rooflines(kernel_cw_iters)
+    valu_roof, lds_roof = onchip_rooflines(kernel_cw_iters, g.kernel_name(False))
     if lds_roof is None:  # no issue-model profile: report the measured HBM use as the roofline
         roof = {"bound": "hbm", "achieved": hbm_model.get("measured_GBps"), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": hbm_model.get("measured_frac")}
