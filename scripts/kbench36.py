@@ -7,7 +7,7 @@ from iib_project_ldpc_codes_amd import decoder
 from iib_project_ldpc_codes_amd.graph import TannerGraph
 g = TannerGraph.random_regular(10000, 3, 6, seed=1)
 B = 65536; it = int(os.environ.get("ITERS", "50")); algo = int(os.environ.get("ALGO", "0"))
-llr = decoder.channel_dev("awgn", 0.85, 2026, 0, g.n, B)
+llr = decoder.channel_dev("awgn", float(os.environ.get("SIGMA", "0.85")), 2026, 0, g.n, B)
 hard = torch.empty(llr.shape, dtype=torch.uint8, device="cuda")
 s = torch.cuda.current_stream()
 cp, cv, vp, vs = [__import__("numpy").ascontiguousarray(x, "int32") for x in g.to_csr()]
