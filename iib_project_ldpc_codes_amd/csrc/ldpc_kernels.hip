@@ -1533,7 +1533,12 @@ constexpr int loc_waves_per_simd(int T, int KP) { return T == 512 && KP <= 5 ? 4
 template <int DLO, int DHI, int DVN0, int DVN1, int KP, int T, int ALGO, bool ABS0, bool ABS1, bool ET = false,
           bool MC = false>
 __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(BpArgs a) {
-    static_assert(!ET || (MC && ALGO == 0), "early stop: sum-product Monte-Carlo only");
+    static_assert(!ET || (MC && (ALGO == 0 || DLO == DHI)), "early stop: Monte-Carlo only (min-sum: one check class)");
+    // MSET (min-sum Monte-Carlo with early stop): min-sum messages carry their own signs, so
+    // the decisions cannot ride in them as in sum-product; instead every change of a
+    // variable's decision XORs its checks' bits of an LDS syndrome (a few atomics once
+    // decoding settles) and the next check phase tests that syndrome
+    constexpr bool MSET = ET && ALGO == 1;
     constexpr int VP = 2 * KP;  // variable pairs per thread
     constexpr int DVM = DVN0 > DVN1 ? DVN0 : DVN1;
     constexpr int DVA = DVM > 0 ? DVM : 1;
@@ -1605,12 +1610,39 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
 
     int *curve = reinterpret_cast<int *>(smem + (((size_t)(a.loc_words + 64 > n ? a.loc_words + 64 : n) * 4 + 15) &
                                                   ~(size_t)15));
+    uint32_t *syn = reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(curve) +
+                                                 (((size_t)(iters + 1) * 4 + 15) & ~(size_t)15));
+    const int nsw = (2 * a.loc_P + 31) >> 5;  // MSET: syndrome words (bit 2q + h: check h of pair q)
+    uint32_t hbits = 0;  // MSET: the thread's current decisions, bits 2v, 2v + 1 of var pair v
+    // MSET: flip the syndrome bits of the checks of var pair v (pair slot k) whose decisions
+    // changed (ch: bit 0 .x, bit 1 .y); b0 / b1: byte addresses of the non-local slots
+    auto syn_flip = [&](auto dn_tag, int k, int ch, const uint32_t (&b0)[DVA], const uint32_t (&b1)[DVA]) {
+        constexpr int DN = decltype(dn_tag)::value;
+        const int q = tid + k * T;
+        if (q >= a.loc_P) return;
+        const uint32_t P4 = 4u * (uint32_t)a.loc_P;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!((ch >> h) & 1)) continue;
+            const uint32_t bl = 2u * (uint32_t)q + (uint32_t)h;
+            atomicXor(&syn[bl >> 5], 1u << (bl & 31));
+#pragma unroll
+            for (int u = 0; u < DN; ++u) {
+                uint32_t w = ((h ? b1[u] : b0[u]) >> 2) - (uint32_t)lpos0;  // W + r 4P + 4i + 2(row%2) + h'
+                w = w >= P4 ? w - P4 : w;
+                const uint32_t bn = 2u * (w >> 2) + (w & 1u);
+                atomicXor(&syn[bn >> 5], 1u << (bn & 31));
+            }
+        }
+    };
     for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
         const uint64_t cw = a.first_cw + (uint64_t)b;
         __syncthreads();  // the previous codeword's outputs are out of LDS
         int err0 = 0;
         if constexpr (MC) {
             for (int i = tid; i <= iters; i += T) curve[i] = 0;
+            if constexpr (MSET)
+                for (int i = tid; i < nsw; i += T) syn[i] = 0u;
             for (int v = tid; v < n; v += T) {
                 const float l = chan_soft(a.ch, cw, v);
                 msg[v] = l * Domain<ALGO>::in;
@@ -1650,6 +1682,17 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                                    __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].y, -126.0f, 126.0f)));
             } else {
                 w = L[v];
+                if constexpr (MSET) {  // the channel decisions' syndrome
+                    const int d0 = (int)(w.x < 0.0f) | ((int)(w.y < 0.0f) << 1);
+                    hbits |= (uint32_t)d0 << (2 * v);
+                    uint32_t b0[DVA], b1[DVA];
+#pragma unroll
+                    for (int u = 0; u < DN; ++u) {
+                        b0[u] = pos_lo_x4(sp[v][u]);
+                        b1[u] = pos_hi_x4(sp[v][u]);
+                    }
+                    if (d0) syn_flip(dn_tag, v >> 1, d0, b0, b1);
+                }
             }
             loc[v] = w;
 #pragma unroll
@@ -1658,6 +1701,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                 at(pos_hi_x4(sp[v][u])) = w.y;
             }
         };
+        hbits = 0u;
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
             init(int_c<DVN0>{}, 2 * k);
@@ -1709,6 +1753,14 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                     at(a1[u]) = s.y - cv[u].y;
                 }
                 loc[v] = make_float2(s.x - loc[v].x, s.y - loc[v].y);
+                if constexpr (MC) dec = (int)(s.x < 0.0f) | ((int)(s.y < 0.0f) << 1);
+                if constexpr (MSET) {
+                    const int ch = dec ^ (int)((hbits >> (2 * v)) & 3u);
+                    if (ch) {
+                        hbits ^= (uint32_t)ch << (2 * v);
+                        syn_flip(dn_tag, v >> 1, ch, a0, a1);
+                    }
+                }
             }
             return dec;
         };
@@ -1729,8 +1781,8 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                 asm volatile("" : "+v"(q));  // recomputed per iteration: no per-pair addresses held live
                 if (q < (LDPC_ABLATE_PHASE == 1 ? 0 : a.loc_P)) {
                     if constexpr (DLO == DHI) {  // one class: rows of P pairs from word 0
-                        unsat |= loc_check_pair<DLO, ALGO, false, ET>(msg, 0, a.loc_P, q, loc[2 * k], loc[2 * k + 1],
-                                                                      a.alpha);
+                        unsat |= loc_check_pair<DLO, ALGO, false, ET && SPA>(msg, 0, a.loc_P, q, loc[2 * k],
+                                                                             loc[2 * k + 1], a.alpha);
                     } else {
                         // class of q by selects on the (scalar) class table -- no per-lane
                         // indexing of kernel arguments
@@ -1743,13 +1795,15 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                             W = in ? a.loc_cls_w[j] : W;
                             d = in ? a.loc_cls_d[j] : d;
                         }
-                        unsat |= loc_check_dispatch<DLO, DHI, ALGO, ET>(d, msg, W, q1 - q0, q - q0, loc[2 * k],
-                                                                        loc[2 * k + 1], a.alpha);
+                        unsat |= loc_check_dispatch<DLO, DHI, ALGO, ET && SPA>(d, msg, W, q1 - q0, q - q0, loc[2 * k],
+                                                                               loc[2 * k + 1], a.alpha);
                     }
                 }
                 if (LDPC_LOC_CGROUP > 0 && k % LDPC_LOC_CGROUP == LDPC_LOC_CGROUP - 1)
                     __builtin_amdgcn_sched_barrier(0);  // pairs in flight (VGPR budget)
             }
+            if constexpr (MSET)
+                for (int i = tid; i < nsw; i += T) unsat |= syn[i] != 0u;
             if constexpr (ET) {
                 // the syndrome of the previous variable phase's decisions: stop when every
                 // check is satisfied (oracle: after that iteration)
@@ -3152,6 +3206,9 @@ enum class BpPath { Loc, Lds36, Irr, Generic8, Generic16, Generic32, GenericG8, 
 #ifndef LDPC_LOC
 #define LDPC_LOC 1  // fixed-count decode on bp_loc_kernel when the graph has a local-edge layout
 #endif
+#ifndef LDPC_LOC_MSMC
+#define LDPC_LOC_MSMC 1  // (3,6) min-sum Monte-Carlo (with or without early stop) on bp_loc_kernel
+#endif
 // bp_loc_kernel shapes: (check-degree range, non-local edges per variable, absent edges)
 // x (threads, check pairs per thread)
 bool loc_shape(const ldpc_graph &g, int &T, int &KP) {
@@ -3167,8 +3224,10 @@ bool loc_shape(const ldpc_graph &g, int &T, int &KP) {
     return (T == 256 && KP >= 1 && KP <= 4) || (T == 1024 && KP >= 2 && KP <= 3) ||
            (T == 512 && (KP == 8 || KP == 10) && rsu) || (T == 512 && KP == 5 && reg36);
 }
-size_t loc_lds_bytes(const ldpc_graph &g, int iters = 0, bool mc = false) {
-    return (((size_t)std::max(g.loc_words + 64, g.n) * 4 + 15) & ~(size_t)15) + (mc ? (size_t)(iters + 1) * 4 : 0);
+// messages | MC: per-iteration curve (16-byte padded) | min-sum MC: syndrome bits
+size_t loc_lds_bytes(const ldpc_graph &g, int iters = 0, bool mc = false, bool syn = false) {
+    return (((size_t)std::max(g.loc_words + 64, g.n) * 4 + 15) & ~(size_t)15) +
+           (mc ? (((size_t)(iters + 1) * 4 + 15) & ~(size_t)15) : 0) + (syn ? (size_t)((g.m + 31) / 32) * 4 : 0);
 }
 
 // bp_irr_kernel: LDS bytes (messages, syndrome bits, curve) and whether the slab is used
@@ -3200,9 +3259,9 @@ BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc, int algo = 
     // (Monte-Carlo with or without early stop: sum-product only; plain early-stop decodes,
     // which return posteriors, stay on the other kernels)
     const bool lds36_ms = LDPC_LDS36_MINSUM && algo == 1 && g.lane_var && g.dv == 3 && g.dc == 6 && g.loc_T != 512;
-    const bool mode_ok = mc ? algo == 0 : !et;
+    const bool mode_ok = mc ? (algo == 0 || (LDPC_LOC_MSMC && g.loc_dlo == 6 && g.loc_dhi == 6)) : !et;
     if (LDPC_LOC && mode_ok && iters > 0 && !lds36_ms && loc_shape(g, lT, lKP) &&
-        loc_lds_bytes(g, iters, mc) <= kLdsMax - 2048)
+        loc_lds_bytes(g, iters, mc, mc && et && algo == 1) <= kLdsMax - 2048)
         return BpPath::Loc;
     if (g.lane_var && g.dv == 3 && g.dc == 6 && lds36_bytes(g, iters, et, mc) <= kLdsMax - 2048)
         return BpPath::Lds36;
@@ -3275,7 +3334,7 @@ hipError_t launch_generic(const ldpc_graph &g, BpArgs a, hipStream_t s) {
 template <int DLO, int DHI, int D0, int D1, bool A0, bool A1, int T, int KP, int ALGO, bool ET, bool MC>
 hipError_t launch_loc_shape(const ldpc_graph &g, const BpArgs &a, hipStream_t s) {
     auto k = bp_loc_kernel<DLO, DHI, D0, D1, KP, T, ALGO, A0, A1, ET, MC>;
-    const size_t lds = loc_lds_bytes(g, a.max_iters, MC);
+    const size_t lds = loc_lds_bytes(g, a.max_iters, MC, MC && ET && ALGO == 1);
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(a.B), dim3(T), lds, s, a);
@@ -3313,7 +3372,8 @@ hipError_t launch_loc(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     }
     for (int i = 0; i < 4; ++i) a.loc_cls_d[i] = g.loc_cls_d[i];
     if (g.loc_dlo == 6) return launch_loc_deg<6, 6, 2, 2, false, false, ALGO, ET, MC>(g, a, T, KP, s);
-    return launch_loc_deg<5, 6, 1, 3, false, true, ALGO, ET, MC>(g, a, T, KP, s);
+    if constexpr (ET && ALGO == 1) return hipErrorInvalidValue;  // min-sum early stop: one check class only
+    else return launch_loc_deg<5, 6, 1, 3, false, true, ALGO, ET, MC>(g, a, T, KP, s);
 }
 
 template <int DC, int VPT, int ALGO, bool ET, bool MC>
@@ -3346,7 +3406,7 @@ template <int ALGO, bool ET, bool MC>
 hipError_t dispatch_bp(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     switch (choose_path(g, a.max_iters, ET, MC, ALGO)) {
         case BpPath::Loc:
-            if constexpr (MC ? ALGO == 0 : !ET) return launch_loc<ALGO, ET, MC>(g, a, s);
+            if constexpr (MC || !ET) return launch_loc<ALGO, ET, MC>(g, a, s);
             return hipErrorInvalidValue;
         case BpPath::Lds36: return launch_lds36<ALGO, ET, MC>(g, a, s);
         case BpPath::Irr: return launch_irr<ALGO, ET, MC>(g, a, s);

@@ -117,3 +117,33 @@ def test_loc_mc_spa_vs_oracle(torch, monkeypatch, kind, n, sigma, early_stop):
     assert abs(int(got[3]) - int(its.sum())) <= 0.005 * its.sum() + 2, (got[:4], int(its.sum()))
     assert got[4] == int((llr < 0).sum())  # channel errors: bit-exact (Philox + fused channel)
     assert got[4 + iters] == got[2]  # the last curve point is the final error count
+
+
+@pytest.mark.parametrize("kind,n", [("reg", 1000), ("reg", 10000)])
+@pytest.mark.parametrize("early_stop", [True, False])
+def test_loc_mc_minsum_exact(torch, monkeypatch, kind, n, early_stop):
+    """Fused Monte-Carlo min-sum on bp_loc_kernel (configs[2]: BSC, normalized min-sum), with the
+    LDS-syndrome early stop (decision changes XOR their checks' syndrome bits): every counter
+    -- frames, frame / bit errors, iterations, the per-iteration error curve -- bit-exact
+    against the oracle's decodes of the same Philox channel frames."""
+    from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
+    g, csr = _graph(kind, n, 25, False, monkeypatch)
+    assert g.kernel_name() == "bp_loc_kernel"
+    B, iters, p = 192, 20, (0.065 if n == 1000 else 0.076)  # failing frames at both lengths
+    mc = MonteCarlo(g, "bsc", p, iters, algo="minsum", alpha=0.75, early_stop=early_stop, seed=8, batch=B)
+    mc.run_batch(0, B)
+    torch.cuda.synchronize()
+    got = mc.counters.cpu().numpy()
+    llr = oracle.channel(oracle.CH_BSC, p, 8, 0, g.n, B)
+    want = np.zeros(4 + iters + 1, np.int64)
+    want[0] = B
+    want[4] = int((llr < 0).sum())
+    for t in range(1, iters + 1):
+        _, h, _ = oracle.bp_decode_batch(csr, llr, t, 1, alpha=0.75, early_stop=early_stop)
+        want[4 + t] = int(h.sum())
+    _, h, its = oracle.bp_decode_batch(csr, llr, iters, 1, alpha=0.75, early_stop=early_stop)
+    want[1] = int(h.any(axis=1).sum())
+    want[2] = int(h.sum())
+    want[3] = int(its.sum())
+    assert 0 < want[1] < B  # both decoded and failed frames at this crossover probability
+    np.testing.assert_array_equal(got, want)
