@@ -390,7 +390,7 @@ def main():
     else:  # the binding unit is the one with the larger fraction
         roof = dict(max((lds_roof, valu_roof), key=lambda r: r["frac"]))
         roof["other_units"] = {r["bound"]: {"frac": r["frac"], "achieved": r["achieved"], "peak": r["peak"],
-                                            "unit": r["unit"]} for r in (lds_roof, valu_roof) if r is not roof}
+                                            "unit": r["unit"]} for r in (lds_roof, valu_roof) if r["bound"] != roof["bound"]}
     roof["traffic"] = hbm_model.get("measured_traffic_bytes_per_launch")
     roof["hbm_model"] = hbm_model
 
