@@ -620,7 +620,7 @@ const char *ldpc_bp_kernel_name(const ldpc_graph *g, int early_stop) {
 // --------------------------- BEC -------------------------------------------
 int ldpc_bec_decode_batch_dev(const ldpc_graph *g, uint8_t *d_words, int B, int max_iters, int32_t *d_errors,
                               int32_t *d_its, void *stream) {
-    LDPC_REQUIRE(g && d_words && d_errors && d_its && B >= 0 && max_iters >= 0, "bad BEC batch arguments");
+    LDPC_REQUIRE(g && (B == 0 || (d_words && d_errors && d_its)) && B >= 0 && max_iters >= 0, "bad BEC batch arguments");
     if (B == 0 || max_iters == 0) {
         if (B && d_its) LDPC_HIP(hipMemsetAsync(d_its, 0, sizeof(int32_t) * B, static_cast<hipStream_t>(stream)));
         return LDPC_OK;
@@ -662,11 +662,11 @@ static int bec_host(const ldpc_graph *g, uint8_t *words, int B, int max_iters, i
 int ldpc_bec_decode_batch(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list, int n,
                           int k, int dv, int dc, uint8_t *words, int B, int max_iters, int32_t *errors,
                           int32_t *its) {
-    LDPC_REQUIRE(words && errors && its && B >= 0 && max_iters >= 0, "bad BEC batch arguments");
+    LDPC_REQUIRE((B == 0 || (words && errors && its)) && B >= 0 && max_iters >= 0, "bad BEC batch arguments");
     ldpc_graph *g = nullptr;
     int rc = ldpc_graph_create(variable_to_check_list, check_to_variable_list, n, k, dv, dc, &g);
     if (rc) return rc;
-    rc = bec_host(g, words, B, max_iters, errors, its);
+    rc = B ? bec_host(g, words, B, max_iters, errors, its) : LDPC_OK;
     ldpc_graph_destroy(g);
     return rc;
 }
@@ -715,7 +715,7 @@ int message_passing(int *Mvc, int iterations, int *variable_to_check_list, int *
 // --------------------------- soft ------------------------------------------
 int ldpc_bp_decode_batch_dev(const ldpc_graph *g, const float *d_llr, int B, int max_iters, int algo, float alpha,
                              int early_stop, float *d_post, uint8_t *d_hard, int32_t *d_its, void *stream) {
-    LDPC_REQUIRE(g && d_llr && B >= 0 && max_iters >= 0, "bad soft batch arguments");
+    LDPC_REQUIRE(g && (B == 0 || d_llr) && B >= 0 && max_iters >= 0, "bad soft batch arguments");
     LDPC_REQUIRE(algo == LDPC_ALGO_SPA || algo == LDPC_ALGO_MINSUM, "algo must be LDPC_ALGO_SPA or LDPC_ALGO_MINSUM");
     if (!g->consistent) {
         set_error("soft decoding needs consistent edge lists (each (v,c) pair listed equally often on both sides)");
@@ -742,10 +742,14 @@ int ldpc_bp_decode_batch_dev(const ldpc_graph *g, const float *d_llr, int B, int
 int ldpc_bp_decode_batch(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list, int n, int k,
                          int dv, int dc, const float *llr, int B, int max_iters, int algo, float alpha,
                          int early_stop, float *post, uint8_t *hard, int32_t *its) {
-    LDPC_REQUIRE(llr && B >= 0, "bad soft batch arguments");
+    LDPC_REQUIRE((B == 0 || llr) && B >= 0, "bad soft batch arguments");
     ldpc_graph *g = nullptr;
     int rc = ldpc_graph_create(variable_to_check_list, check_to_variable_list, n, k, dv, dc, &g);
     if (rc) return rc;
+    if (B == 0) {  // validated graph, nothing to decode
+        ldpc_graph_destroy(g);
+        return LDPC_OK;
+    }
     {
         std::lock_guard<std::mutex> lk(g_mu);
         Workspace &ws = workspace(nullptr);
@@ -802,10 +806,11 @@ static int channel_params(int channel, float param, float *p, float *p2) {
 
 int ldpc_channel_dev(int channel, float param, uint64_t seed, uint64_t first_cw, int n, int B, void *d_out,
                      void *stream) {
-    LDPC_REQUIRE(d_out && n > 0 && B >= 0, "bad channel arguments");
+    LDPC_REQUIRE((B == 0 || d_out) && n > 0 && B >= 0, "bad channel arguments");
     float p, p2;
     int rc = channel_params(channel, param, &p, &p2);
     if (rc) return rc;
+    if (B == 0) return LDPC_OK;
     LDPC_HIP(launch_channel(channel, p, p2, seed, first_cw, n, B, d_out, static_cast<hipStream_t>(stream)));
     return LDPC_OK;
 }
@@ -995,7 +1000,7 @@ static int ml_check_shape(int n, int m) {
 
 int ldpc_ml_decode_batch_dev(const ldpc_graph *g, const uint8_t *d_words, int B, uint8_t *d_out,
                              int32_t *d_unsolved, void *stream) {
-    LDPC_REQUIRE(g && d_words && d_out && d_unsolved && B >= 0, "bad ML batch arguments");
+    LDPC_REQUIRE(g && (B == 0 || (d_words && d_out && d_unsolved)) && B >= 0, "bad ML batch arguments");
     int rc = ml_check_shape(g->n, g->m);
     if (rc) return rc;
     if (B == 0) return LDPC_OK;
@@ -1005,7 +1010,7 @@ int ldpc_ml_decode_batch_dev(const ldpc_graph *g, const uint8_t *d_words, int B,
 }
 
 int ldpc_ml_decode_batch(const ldpc_graph *g, const uint8_t *words, int B, uint8_t *out, int32_t *unsolved) {
-    LDPC_REQUIRE(g && words && out && unsolved && B >= 0, "bad ML batch arguments");
+    LDPC_REQUIRE(g && (B == 0 || (words && out && unsolved)) && B >= 0, "bad ML batch arguments");
     int rc = ml_check_shape(g->n, g->m);
     if (rc) return rc;
     if (B == 0) return LDPC_OK;
@@ -1029,7 +1034,7 @@ int ldpc_ml_ensemble_decode_dev(int n, int dv, int dc, const int32_t *d_check_lo
                                 uint8_t *d_out, int32_t *d_unsolved, void *stream) {
     int rc = check_regular_shape(n, dv, dc);
     if (rc) return rc;
-    LDPC_REQUIRE(d_check_lookup && d_words && d_out && d_unsolved && B >= 0, "bad ML batch arguments");
+    LDPC_REQUIRE((B == 0 || (d_check_lookup && d_words && d_out && d_unsolved)) && B >= 0, "bad ML batch arguments");
     rc = ml_check_shape(n, n * dv / dc);
     if (rc) return rc;
     rc = require_device();

@@ -12,6 +12,11 @@
  * (LDPC_E*); ldpc_last_error() returns a human-readable message.  The drop-in
  * message_passing keeps the reference's convention (returns the iteration
  * index) and returns a negative LDPC_E* code on failure.
+ *
+ * Empty batches: B = 0 is a no-op returning LDPC_OK (after the graph and
+ * shape checks); the per-codeword buffers may then be NULL (an empty device
+ * tensor's data pointer).  max_iters = 0: BEC words are left as they are with
+ * its = 0; soft decoders return the channel LLRs as posteriors.
  */
 #ifndef LDPC_MI355X_H
 #define LDPC_MI355X_H
