@@ -117,6 +117,13 @@ def cpu_baseline(graph, llr_host, seconds):
            "host": detail,
            "single_core": {"value": done_one / el_one, "unit": "codewords/s", "cores": 1,
                            "sample": f"{done_one} frames in {el_one:.1f} s"}}
+    if total != cores:
+        # one thread per CPU os.cpu_count() reports, for the record: the job's cgroup quota caps
+        # what they can use, so this is not more compute than `value`'s `cores` threads
+        done_os, el_os = spa(total, seconds * 0.15)
+        out["os_cpu_count_threads"] = {"value": done_os / el_os, "unit": "codewords/s", "threads": total,
+                                       "cgroup_quota_cpus": detail["cgroup_quota_cpus"],
+                                       "sample": f"{done_os} frames in {el_os:.1f} s"}
     # the reference hot path itself: message_passing.c at configs[0] (n=1000, eps=0.4, 50 iterations)
     gb = graph_cfg0()
     words = oracle.channel(oracle.CH_BEC, 0.40, 5, 0, gb.n, 4096)
@@ -354,6 +361,23 @@ def main():
         torch.cuda.synchronize()
         cnt = mc.counters.cpu().numpy()
         extras["irregular_cfg4_mc_sigma0.84_early_stop"] = {
+            "trials_per_s": Bm / (a.elapsed_time(b) * 1e-3), "batch": Bm, "mean_iterations": float(cnt[3] / cnt[0]),
+            "fer": float(cnt[1] / cnt[0])}
+        # configs[2] shape: BSC normalized min-sum Monte-Carlo, (3,6) n = 10,000 (fused channel,
+        # LDS-syndrome early stop, 50 iterations), p = 0.07.  The code is the headline law's seed-1
+        # draw with distinct columns (scripts/fer_sweep.py cfg3): the plain draw holds one pair of
+        # identical columns, a weight-2 codeword that one channel flip turns into a tie (FER 2p(1-p))
+        gd = TannerGraph.random_regular(N_BITS, DV, DC, seed=1, distinct_columns=True)
+        Bm = 65536
+        mc = MonteCarlo(gd, "bsc", 0.07, ITERS, algo="minsum", alpha=0.75, early_stop=True, seed=11, batch=Bm)
+        mc.run_batch(0, Bm)
+        torch.cuda.synchronize()
+        a.record(stream)
+        mc.run_batch(Bm, Bm)
+        b.record(stream)
+        torch.cuda.synchronize()
+        cnt = mc.counters.cpu().numpy()
+        extras["bsc_minsum_mc_cfg2_p0.07_early_stop"] = {
             "trials_per_s": Bm / (a.elapsed_time(b) * 1e-3), "batch": Bm, "mean_iterations": float(cnt[3] / cnt[0]),
             "fer": float(cnt[1] / cnt[0])}
         # "optimal" modes: ML erasure decoding (parallel_simulator.py:60-129), n = 1000, eps = 0.45
