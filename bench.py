@@ -295,7 +295,17 @@ def main():
         torch.cuda.synchronize()
         et_ms = a.elapsed_time(b)
         extras["early_stop_spa"] = {"codewords_per_s": B / (et_ms * 1e-3),
-                                    "mean_iterations": float(its.float().mean().item())}
+                                    "mean_iterations": float(its.float().mean().item()),
+                                    "kernel": g.kernel_name(early_stop=True)}
+        # the same with hard decisions only (no posteriors): the local-edge kernel
+        a.record(stream)
+        decoder.bp_decode_dev(g, llr, ITERS, "spa", early_stop=True, post=None, hard=hard, its=its, stream=stream,
+                              want_post=False)
+        b.record(stream)
+        torch.cuda.synchronize()
+        extras["early_stop_spa_hard_only"] = {"codewords_per_s": B / (a.elapsed_time(b) * 1e-3),
+                                              "mean_iterations": float(its.float().mean().item()),
+                                              "kernel": g.kernel_name(early_stop=True, hard_only=True)}
         a.record(stream)
         decoder.bp_decode_dev(g, llr, ITERS, "minsum", alpha=0.75, post=post, hard=hard, its=its, stream=stream)
         b.record(stream)
@@ -348,7 +358,7 @@ def main():
             torch.cuda.synchronize()
             extras[key] = {"codewords_per_s": Bi / (a.elapsed_time(b) * 1e-3), "batch": Bi, "sigma": 0.80,
                            "mean_iterations": float(its_i.float().mean().item()),
-                           "kernel": gi.kernel_name(early_stop=et)}
+                           "kernel": gi.kernel_name(early_stop=et, hard_only=True)}
         del llr_i
         # configs[3] Monte-Carlo as scripts/fer_sweep.py runs it (fused channel, sign-bit early stop)
         Bm = 65536

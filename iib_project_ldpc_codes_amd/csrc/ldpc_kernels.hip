@@ -1525,7 +1525,10 @@ template <bool B> using bool_c = std::integral_constant<bool, B>;
 // variable of that slot has fewer (its absent edges gather the neutral value).
 // MC (sum-product): fused Philox channel, per-iteration error counts of the all-zero
 // codeword into the trial curve, no posteriors; ET with MC: syndrome early stop on the
-// sign-bit decisions (see loc_check_pair).
+// sign-bit decisions (see loc_check_pair).  ET without MC (hard-decision decodes: the caller
+// asked for no posteriors): the same stop, the decisions of the stopping iteration kept in a
+// bit per variable (hbits) and written out; a frame that never stops takes the fixed-count
+// epilogue.
 // 512 threads with up to 5 check pairs each: two workgroups per CU (4 waves per SIMD, <= 128
 // VGPRs), so one workgroup's barrier waits overlap the other's work; else one workgroup
 constexpr int loc_waves_per_simd(int T, int KP) { return T == 512 && KP <= 5 ? 4 : 1; }
@@ -1533,7 +1536,8 @@ constexpr int loc_waves_per_simd(int T, int KP) { return T == 512 && KP <= 5 ? 4
 template <int DLO, int DHI, int DVN0, int DVN1, int KP, int T, int ALGO, bool ABS0, bool ABS1, bool ET = false,
           bool MC = false>
 __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(BpArgs a) {
-    static_assert(!ET || (MC && (ALGO == 0 || DLO == DHI)), "early stop: Monte-Carlo only (min-sum: one check class)");
+    static_assert(!ET || ALGO == 0 || DLO == DHI, "min-sum early stop: one check class");
+    static_assert(!ET || 2 * 2 * KP <= 64, "early stop keeps the thread's decisions in one 64-bit word");
     // MSET (min-sum Monte-Carlo with early stop): min-sum messages carry their own signs, so
     // the decisions cannot ride in them as in sum-product; instead every change of a
     // variable's decision XORs its checks' bits of an LDS syndrome (a few atomics once
@@ -1613,7 +1617,10 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     uint32_t *syn = reinterpret_cast<uint32_t *>(reinterpret_cast<unsigned char *>(curve) +
                                                  (((size_t)(iters + 1) * 4 + 15) & ~(size_t)15));
     const int nsw = (2 * a.loc_P + 31) >> 5;  // MSET: syndrome words (bit 2q + h: check h of pair q)
-    uint32_t hbits = 0;  // MSET: the thread's current decisions, bits 2v, 2v + 1 of var pair v
+    // MSET / hard-decision ET: the thread's current decisions, bits 2v, 2v + 1 of var pair v
+    using HB = std::conditional_t<(4 * KP > 32), uint64_t, uint32_t>;
+    static_assert(!MSET || sizeof(HB) == 4, "MSET: 32-bit decision word");
+    HB hbits = 0;
     // MSET: flip the syndrome bits of the checks of var pair v (pair slot k) whose decisions
     // changed (ch: bit 0 .x, bit 1 .y); b0 / b1: byte addresses of the non-local slots
     auto syn_flip = [&](auto dn_tag, int k, int ch, const uint32_t (&b0)[DVA], const uint32_t (&b1)[DVA]) {
@@ -1649,6 +1656,8 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                 err0 += (l < 0.0f);
             }
         } else {
+            if constexpr (MSET)
+                for (int i = tid; i < nsw; i += T) syn[i] = 0u;
             for (int v = tid; v < n; v += T) msg[v] = a.llr[(size_t)b * n + v] * Domain<ALGO>::in;
         }
         __syncthreads();
@@ -1723,13 +1732,14 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
 #pragma unroll
                 for (int j = 2; j < DV; ++j) pre[j] = pre[j - 1] * cv[j - 2];
                 uint32_t sx = 0, sy = 0;  // ET: the decision rides in every outgoing sign bit
-                if constexpr (MC) {
+                if constexpr (MC || ET) {
                     const float2 P = DN > 0 ? pre[DV - 1] * cv[DN > 0 ? DN - 1 : 0] : pre[DV - 1];
                     dec = (int)(P.x < 1.0f) | ((int)(P.y < 1.0f) << 1);
                     if constexpr (ET) {
                         sx = (uint32_t)(dec & 1) << 31;
                         sy = (uint32_t)(dec >> 1) << 31;
                     }
+                    if constexpr (ET && !MC) hbits = (hbits & ~((HB)3 << (2 * v))) | ((HB)dec << (2 * v));
                 }
                 auto sgn = [&](float2 R) {
                     if constexpr (ET) return make_float2(__uint_as_float(__float_as_uint(R.x) | sx),
@@ -1753,7 +1763,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                     at(a1[u]) = s.y - cv[u].y;
                 }
                 loc[v] = make_float2(s.x - loc[v].x, s.y - loc[v].y);
-                if constexpr (MC) dec = (int)(s.x < 0.0f) | ((int)(s.y < 0.0f) << 1);
+                if constexpr (MC || ET) dec = (int)(s.x < 0.0f) | ((int)(s.y < 0.0f) << 1);
                 if constexpr (MSET) {
                     const int ch = dec ^ (int)((hbits >> (2 * v)) & 3u);
                     if (ch) {
@@ -1765,6 +1775,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             return dec;
         };
         int it = 0;
+        bool stopped = false;
         for (; it < iters; ++it) {
             __syncthreads();  // variable phase (or initialisation) complete
             int unsat = 0;
@@ -1807,7 +1818,10 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             if constexpr (ET) {
                 // the syndrome of the previous variable phase's decisions: stop when every
                 // check is satisfied (oracle: after that iteration)
-                if (!__syncthreads_or(unsat | (it == 0))) break;
+                if (!__syncthreads_or(unsat | (it == 0))) {
+                    stopped = true;
+                    break;
+                }
             } else {
                 __syncthreads();
             }
@@ -1836,6 +1850,21 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             for (int i = tid; i <= iters; i += T) tr[i] = i <= it ? curve[i] : last;
             if (tid == 0) a.its[b] = it;
             continue;
+        }
+        if constexpr (ET) {
+            if (stopped) {  // hard decisions of the stopping iteration (no posteriors asked for)
+#pragma unroll
+                for (int v = 0; v < VP; ++v) {
+                    const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid), v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
+                    if (v0 >= 0) msg[v0] = (hbits >> (2 * v)) & 1 ? -1.0f : 1.0f;
+                    if (v1 >= 0) msg[v1] = (hbits >> (2 * v + 1)) & 1 ? -1.0f : 1.0f;
+                }
+                __syncthreads();
+                if (a.hard)
+                    for (int v = tid; v < n; v += T) a.hard[(size_t)b * n + v] = (uint8_t)(msg[v] < 0.0f);
+                if (a.its && tid == 0) a.its[b] = it;
+                continue;
+            }
         }
         // ---- posteriors (after the last check phase) and outputs ----
         // (variable ids re-read where needed: not kept live through the decode loop)
@@ -3209,6 +3238,9 @@ enum class BpPath { Loc, Lds36, Irr, Generic8, Generic16, Generic32, GenericG8, 
 #ifndef LDPC_LOC_MSMC
 #define LDPC_LOC_MSMC 1  // (3,6) min-sum Monte-Carlo (with or without early stop) on bp_loc_kernel
 #endif
+#ifndef LDPC_LOC_HARD_ET
+#define LDPC_LOC_HARD_ET 1  // early-stop decodes without posteriors on bp_loc_kernel
+#endif
 // bp_loc_kernel shapes: (check-degree range, non-local edges per variable, absent edges)
 // x (threads, check pairs per thread)
 bool loc_shape(const ldpc_graph &g, int &T, int &KP) {
@@ -3249,19 +3281,23 @@ size_t generic_lds_bytes(const ldpc_graph &g, int iters, bool mc) {
     return (((size_t)g.E * 5 + (size_t)g.n * 4 + 15) & ~(size_t)15) + (mc ? (size_t)(iters + 1) * 4 : 0);
 }
 
-BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc, int algo = 0) {
+BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc, int algo = 0, bool hard_only = false) {
     if (!g.consistent) return BpPath::None;
     int lT = 0, lKP = 0;
     // min-sum on (3,6) codes with one 1024-thread local-edge workgroup per CU: bp_lds_kernel
     // is faster (its variable sums need no reordering); with the two-workgroup 512-thread
     // shape the local-edge kernel wins (bench code: 2.00 vs 1.74 M cw/s); the local-edge
     // kernel for everything else it covers
-    // (Monte-Carlo with or without early stop: sum-product only; plain early-stop decodes,
-    // which return posteriors, stay on the other kernels)
+    // (Monte-Carlo with or without early stop; early-stop decodes that return posteriors stay
+    // on the other kernels, hard-decision-only ones run here; min-sum early stop: one check
+    // class)
     const bool lds36_ms = LDPC_LDS36_MINSUM && algo == 1 && g.lane_var && g.dv == 3 && g.dc == 6 && g.loc_T != 512;
-    const bool mode_ok = mc ? (algo == 0 || (LDPC_LOC_MSMC && g.loc_dlo == 6 && g.loc_dhi == 6)) : !et;
+    const bool one_cls = g.loc_dlo == 6 && g.loc_dhi == 6;
+    const bool mode_ok = mc ? (algo == 0 || (LDPC_LOC_MSMC && one_cls))
+                            : (!et || (LDPC_LOC_HARD_ET && hard_only && (algo == 0 || one_cls)));
+    const bool mset = et && algo == 1;
     if (LDPC_LOC && mode_ok && iters > 0 && !lds36_ms && loc_shape(g, lT, lKP) &&
-        loc_lds_bytes(g, iters, mc, mc && et && algo == 1) <= kLdsMax - 2048)
+        loc_lds_bytes(g, iters, mc || mset, mset) <= kLdsMax - 2048)
         return BpPath::Loc;
     if (g.lane_var && g.dv == 3 && g.dc == 6 && lds36_bytes(g, iters, et, mc) <= kLdsMax - 2048)
         return BpPath::Lds36;
@@ -3334,7 +3370,7 @@ hipError_t launch_generic(const ldpc_graph &g, BpArgs a, hipStream_t s) {
 template <int DLO, int DHI, int D0, int D1, bool A0, bool A1, int T, int KP, int ALGO, bool ET, bool MC>
 hipError_t launch_loc_shape(const ldpc_graph &g, const BpArgs &a, hipStream_t s) {
     auto k = bp_loc_kernel<DLO, DHI, D0, D1, KP, T, ALGO, A0, A1, ET, MC>;
-    const size_t lds = loc_lds_bytes(g, a.max_iters, MC, MC && ET && ALGO == 1);
+    const size_t lds = loc_lds_bytes(g, a.max_iters, MC || (ET && ALGO == 1), ET && ALGO == 1);
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(a.B), dim3(T), lds, s, a);
@@ -3404,10 +3440,8 @@ hipError_t launch_irr(const ldpc_graph &g, BpArgs a, hipStream_t s) {
 
 template <int ALGO, bool ET, bool MC>
 hipError_t dispatch_bp(const ldpc_graph &g, BpArgs a, hipStream_t s) {
-    switch (choose_path(g, a.max_iters, ET, MC, ALGO)) {
-        case BpPath::Loc:
-            if constexpr (MC || !ET) return launch_loc<ALGO, ET, MC>(g, a, s);
-            return hipErrorInvalidValue;
+    switch (choose_path(g, a.max_iters, ET, MC, ALGO, a.post == nullptr)) {
+        case BpPath::Loc: return launch_loc<ALGO, ET, MC>(g, a, s);
         case BpPath::Lds36: return launch_lds36<ALGO, ET, MC>(g, a, s);
         case BpPath::Irr: return launch_irr<ALGO, ET, MC>(g, a, s);
         case BpPath::Generic8: return launch_generic<8, ALGO, ET, MC, false>(g, a, s);
@@ -3479,7 +3513,8 @@ size_t bp_scratch_bytes(const ldpc_graph &g, int B) {
 }
 
 const char *bp_kernel_name(const ldpc_graph &g, int early_stop) {
-    switch (choose_path(g, 50, early_stop != 0, false)) {
+    // early_stop 2: early stop, hard decisions only (no posteriors)
+    switch (choose_path(g, 50, early_stop != 0, false, 0, early_stop == 2)) {
         case BpPath::Loc: return "bp_loc_kernel";
         case BpPath::Lds36: return "bp_lds_kernel<3,6>";
         case BpPath::Irr: return irr_slab(g) ? "bp_irr_kernel<lds+slab>" : "bp_irr_kernel<lds>";

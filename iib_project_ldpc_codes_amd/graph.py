@@ -135,8 +135,10 @@ class TannerGraph:
         self._handles[dev] = out
         return out
 
-    def kernel_name(self, early_stop=False):
-        return _native.lib().ldpc_bp_kernel_name(self.handle(), int(bool(early_stop))).decode()
+    def kernel_name(self, early_stop=False, hard_only=False):
+        """The soft kernel a decode of this graph runs (hard_only: early stop without posteriors)."""
+        es = (2 if hard_only else 1) if early_stop else 0
+        return _native.lib().ldpc_bp_kernel_name(self.handle(), es).decode()
 
     def __del__(self):
         try:

@@ -108,6 +108,9 @@ int ldpc_bec_decode_batch_dev(const ldpc_graph *g, uint8_t *d_words, int B, int 
  * post float[B*n] (may be NULL), hard decisions hard uint8[B*n] (may be NULL,
  * 1 where post < 0) and iterations run its int32[B] (may be NULL).
  * early_stop != 0 stops a codeword once its hard decision satisfies every check.
+ * With early stop and post == NULL only the stopping iteration's decisions and
+ * the iteration counts are produced, which lets the decode run on the
+ * local-edge kernel (same decisions and counts as the posterior-returning path).
  */
 int ldpc_bp_decode_batch(const int32_t *variable_to_check_list, const int32_t *check_to_variable_list,
                          int n, int k, int dv, int dc, const float *llr, int B, int max_iters,
@@ -312,7 +315,8 @@ int ldpc_debug_loc_layout(const int32_t *check_ptr, const int32_t *check_var, co
                           const int32_t *var_slot, int n, int m, int T, int32_t *shape, int32_t *var, int32_t *pos,
                           int32_t *info);
 
-/* Name of the soft kernel a graph dispatches to (tests / bench). */
+/* Name of the soft kernel a graph dispatches to (tests / bench); early_stop: 0 fixed count,
+ * 1 early stop with posteriors, 2 early stop with hard decisions only (d_post == NULL). */
 const char *ldpc_bp_kernel_name(const ldpc_graph *g, int early_stop);
 
 /* ---------------------------------------------------------------------- */

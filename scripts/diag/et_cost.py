@@ -18,12 +18,13 @@ B = 65536
 s = torch.cuda.current_stream()
 
 
-def timed(llr, iters, algo, es):
+def timed(llr, iters, algo, es, want_post=True):
     ts = []
     for _ in range(3):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(s)
-        post, hard, its = decoder.bp_decode_dev(g, llr, iters, algo, 0.75 if algo == "minsum" else 1.0, es, stream=s)
+        post, hard, its = decoder.bp_decode_dev(g, llr, iters, algo, 0.75 if algo == "minsum" else 1.0, es, stream=s,
+                                                want_post=want_post)
         b.record(s)
         torch.cuda.synchronize()
         ts.append(a.elapsed_time(b))
@@ -46,3 +47,7 @@ for sigma in (0.85, 0.70):
                           "wg512_max_over_mean": float(it.reshape(-1, 512).sum(0).max() / it.reshape(-1, 512).sum(0).mean()),
                           "wg256_max_over_mean": float(it.reshape(-1, 256).sum(0).max() / it.reshape(-1, 256).sum(0).mean())}),
               flush=True)
+        ms, its = timed(llr, 50, algo, True, want_post=False)
+        print(json.dumps({"sigma": sigma, "algo": algo, "es": "hard_only", "iters": 50, "ms": round(ms, 3),
+                          "mean_its": float(its.float().mean().item()),
+                          "kernel": g.kernel_name(early_stop=True, hard_only=True)}), flush=True)
