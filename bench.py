@@ -13,7 +13,7 @@ Weak scaling: every rank decodes its own 65536-frame batch.
 Rank 0 prints one JSON line.  roofline: the decode kernel keeps every edge
 message in LDS, so its binding unit is on-chip: LDS cycles (per CU) or VALU
 issue cycles (per SIMD) per codeword-iteration from the committed HEAD issue
-model (profiles/r02d_issue_model.json, scripts/issue_model.py) x the live
+model (profiles/r02e_issue_model.json, scripts/issue_model.py) x the live
 codeword-iteration rate of the kernel (HIP events on the launch stream) over
 the unit's peak; the larger fraction is `roofline`.  roofline.hbm_model
 keeps SURVEY.md 8(d)'s streaming byte model (2*E*4 + 2*n*4 = 320,000 B per
@@ -169,13 +169,13 @@ def graph_cfg0():
     return TannerGraph.random_regular(1000, DV, DC, seed=1)
 
 
-ISSUE_PROFILE = os.path.join(ROOT, "profiles", "r02d_issue_model.json")
+ISSUE_PROFILE = os.path.join(ROOT, "profiles", "r02e_issue_model.json")
 SIMDS, CUS, CLOCK_HZ = 1024, 256, 2.4e9
 
 
 def onchip_rooflines(cw_iters_per_s, kernel):
     """The units the LDS-resident kernel can saturate, from the committed HEAD issue model
-    (profiles/r02d_issue_model.json, scripts/issue_model.py: the kernel ISA's blocks x their
+    (profiles/r02e_issue_model.json, scripts/issue_model.py: the kernel ISA's blocks x their
     execution counts, cross-checked with and completed by the PMC counters of one launch):
       valu: issue cycles per codeword-iteration (packed f32 4, plain 2, transcendental 8 per
             wave64 instruction, MI355X_MICROARCH.md) over 1024 SIMDs x 2.4 GHz;
@@ -208,7 +208,7 @@ def onchip_rooflines(cw_iters_per_s, kernel):
 
 
 def load_traffic():
-    for name in ("r02d_pmc_traffic.json", "r02c_pmc_traffic.json", "pmc_traffic.json"):
+    for name in ("r02e_pmc_traffic.json", "r02d_pmc_traffic.json", "pmc_traffic.json"):
         p = os.path.join(ROOT, "profiles", name)
         if os.path.exists(p):
             with open(p) as f:
