@@ -771,7 +771,8 @@ int ldpc_bp_decode_batch(const int32_t *variable_to_check_list, const int32_t *c
         // scratch taken inside the _dev call (needs the lock released)
         if (e == hipSuccess) e = ws.scratch.ensure(bp_scratch_bytes(*g, B));
         if (B > 0) {
-            e = launch_bp_decode(*g, dl, B, max_iters, algo, alpha, early_stop, dp, dh, di, nullptr,
+            // no posteriors asked for: early stop may take the hard-decision path (bp_loc_kernel)
+            e = launch_bp_decode(*g, dl, B, max_iters, algo, alpha, early_stop, post ? dp : nullptr, dh, di, nullptr,
                                  static_cast<float *>(ws.scratch.p));
             if (e == hipSuccess) e = hipDeviceSynchronize();
             if (e == hipSuccess && post) e = hipMemcpy(post, dp, nb * 4, hipMemcpyDeviceToHost);

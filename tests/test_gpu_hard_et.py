@@ -77,3 +77,20 @@ def test_spa_hard_early_stop_vs_oracle_and_posterior_path(torch, kind, n, sigma)
     stopped = its < 50
     assert stopped.any() and np.all(_syndrome_ok(csr, hard)[stopped])
     assert np.all(its >= 1)
+
+
+def test_host_form_without_posteriors_matches_device_hard_path(torch):
+    """ldpc_bp_decode_batch (host pointers) with post = NULL takes the same hard-decision path."""
+    from iib_project_ldpc_codes_amd import _native
+    g, _ = _graph("reg", 10000)
+    llr = oracle.channel(oracle.CH_AWGN, 0.85, 19, 0, g.n, 64)
+    dhard, dits = _decode(torch, g, llr, 50, "spa", False)
+    hard = np.zeros_like(dhard)
+    its = np.zeros(64, np.int32)
+    v2c = np.ascontiguousarray(g.variable_lookup, np.int32)
+    c2v = np.ascontiguousarray(g.check_lookup, np.int32)
+    rc = _native.lib().ldpc_bp_decode_batch(v2c.ctypes.data, c2v.ctypes.data, g.n, g.k, 3, 6, llr.ctypes.data, 64,
+                                            50, 0, 1.0, 1, None, hard.ctypes.data, its.ctypes.data)
+    _native.check(rc, "ldpc_bp_decode_batch")
+    np.testing.assert_array_equal(hard, dhard)
+    np.testing.assert_array_equal(its, dits)
