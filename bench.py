@@ -37,16 +37,88 @@ ITERS = 50
 BATCH = 65536
 SIGMA = 0.85
 HBM_PEAK_GBPS = 8000.0
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU); without torchrun's WORLD_SIZE, bench.py starts them itself")
+    ap.add_argument("--rehearse-on-one-gpu", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks share devices, gloo collectives): "
+                         "a rehearsal of the N-rank path on a one-GPU box, not a scaling measurement")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launch_plan(gpus, env, visible, rehearse=False):
+    """How this invocation runs, decided BEFORE anything initialises HIP:
+      ("single", None)  one process, one GPU (--gpus 1, no WORLD_SIZE)
+      ("rank", None)    a rank of an external launcher (torchrun: WORLD_SIZE == --gpus)
+      ("spawn", envs)   bench.py starts --gpus ranks itself, one child process per GPU, with
+                        these environments (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*)
+      ("error", msg)    refused (never a 1-GPU line for --gpus N)
+    visible = GPUs this process can see (torch.cuda.device_count(), which does not
+    initialise the runtime on this image)."""
+    if gpus < 1:
+        return "error", f"--gpus {gpus}: need at least one GPU"
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            return "error", f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks"
+        if not rehearse and gpus > visible:
+            return "error", f"--gpus {gpus} but only {visible} GPU(s) visible"
+        return "rank", None
+    if gpus > visible and not rehearse:
+        return "error", (f"--gpus {gpus} but only {visible} GPU(s) visible to this process "
+                         f"(use --rehearse-on-one-gpu to rehearse the {gpus}-rank path on fewer devices)")
+    if gpus == 1:
+        return "single", None
+    port = env.get("MASTER_PORT") or str(_free_port())
+    envs = []
+    for r in range(gpus):
+        e = dict(env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(gpus), "LOCAL_WORLD_SIZE": str(gpus),
+                  "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port})
+        if rehearse:
+            e["LDPC_DIST_BACKEND"] = "gloo"  # ranks share a device: RCCL needs one rank per GPU
+        envs.append(e)
+    return "spawn", envs
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(envs, argv, script=None):
+    """Start one child process per rank (never exec: this process has not touched the GPU,
+    and stays the parent); rank 0's stdout (the JSON line) passes through.  Returns the
+    worst exit code; if a rank fails the others are terminated."""
+    import subprocess
+    script = script or os.path.abspath(__file__)
+    procs = [subprocess.Popen([sys.executable, "-u", script] + list(argv), env=e) for e in envs]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                c = p.poll()
+                if c is None:
+                    continue
+                procs.remove(p)
+                if c != 0:
+                    rc = rc or c
+                    for q in procs:  # a failed rank: the others would wait in a collective forever
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
 
 
 def host_cores():
@@ -221,6 +293,12 @@ def load_traffic():
 def main():
     args = parse()
     import torch
+    mode, info = launch_plan(args.gpus, os.environ, torch.cuda.device_count(), args.rehearse_on_one_gpu)
+    if mode == "error":
+        print(f"bench.py: {info}", file=sys.stderr, flush=True)
+        return 2
+    if mode == "spawn":
+        return spawn_ranks(info, sys.argv[1:])
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -275,7 +353,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
 
-    fer = float(hard.any(dim=1).float().mean().item())
+    # one collective over all ranks after the timed region: the frame errors of every rank's
+    # own batch (RCCL over xGMI with the nccl backend) -- proves all N ranks joined and decoded
+    fe_local = hard.any(dim=1).sum().to(torch.int64).reshape(1)
+    fe_all, ranks_joined = int(fe_local.item()), 1
+    if world > 1:
+        vec = torch.stack([fe_local[0], torch.ones((), dtype=torch.int64, device=fe_local.device)])
+        if backend != "nccl":
+            vec = vec.cpu()
+        dist.all_reduce(vec)
+        fe_all, ranks_joined = int(vec[0]), int(vec[1])
+    fer = fe_all / (world * B)
     total_cw = world * B * args.steps
     value = total_cw / elapsed
     b_it = 2 * E * 4 + 2 * g.n * 4
@@ -284,7 +372,7 @@ def main():
     traffic = load_traffic()
 
     extras = {}
-    if not args.no_extras and rank == 0:
+    if not args.no_extras and rank == 0 and world == 1:  # the N = 1 line carries the extras
         # same frames with syndrome early termination (max 50 iterations)
         decoder.bp_decode_dev(g, llr, ITERS, "spa", early_stop=True, post=post, hard=hard, its=its, stream=stream)
         torch.cuda.synchronize()
@@ -434,6 +522,11 @@ def main():
             "value": value,
             "unit": "codewords/s",
             "n_gpus": world,
+            "rccl_ranks": ranks_joined if (world > 1 and backend == "nccl") else None,
+            "dist": {"ranks_joined": ranks_joined, "backend": backend if world > 1 else None,
+                     "devices_visible": torch.cuda.device_count(),
+                     "rehearsal_shared_gpu": bool(args.rehearse_on_one_gpu and world > torch.cuda.device_count()),
+                     "frame_errors_all_ranks": fe_all},
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -463,4 +556,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -29,7 +29,8 @@
 namespace ldpc {
 namespace {
 thread_local std::string g_err;
-std::mutex g_mu;  // workspaces and the drop-in graph cache
+std::mutex g_mu;     // the drop-in graph cache and the host-buffer entry points
+std::mutex g_ws_mu;  // the workspace map (each workspace has its own lock)
 
 // Grow-only device buffer.
 struct DevBuf {
@@ -46,7 +47,10 @@ struct DevBuf {
     }
 };
 
+// Lock order: g_mu before Workspace::mu; the device-pointer Monte-Carlo entry takes only its
+// workspace's lock, so launches on different devices / streams never serialise on g_mu.
 struct Workspace {
+    std::mutex mu;
     DevBuf trial, its, cutoff, scratch, words, llr, post, hard, errors, itsb, gchk, gvar, gatt, mlw, mlo, mlu, shape;
 };
 std::map<std::pair<int, void *>, Workspace> g_ws;  // (device, stream)
@@ -54,7 +58,8 @@ std::map<std::pair<int, void *>, Workspace> g_ws;  // (device, stream)
 Workspace &workspace(void *stream) {
     int dev = 0;
     (void)hipGetDevice(&dev);
-    return g_ws[std::make_pair(dev, stream)];
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    return g_ws[std::make_pair(dev, stream)];  // std::map nodes never move
 }
 }  // namespace
 
@@ -430,13 +435,7 @@ int device_graph(const HostGraph &h, ldpc_graph **out) {
             g->loc_T = L.T; g->loc_KP = L.KP; g->loc_DVN = L.DVN; g->loc_P = L.P;
             g->loc_ncls = L.ncls; g->loc_words = L.words;
             int dlo = 99, dhi = 0;
-            bool mix_ok = true;
-            for (int i = 0; i < L.ncls; ++i) {
-                dlo = std::min(dlo, L.cls_d[i] >> 8 ? L.cls_d[i] >> 8 : L.cls_d[i]);
-                dhi = std::max(dhi, L.cls_d[i] & 255);
-            }
-            for (int i = 0; i < L.ncls; ++i)  // the kernel pads a mixed pair's smaller check by one input
-                if (L.cls_d[i] >> 8) mix_ok &= (L.cls_d[i] & 255) == dhi && (L.cls_d[i] >> 8) == dhi - 1;
+            const bool mix_ok = loc_degree_range(L, dlo, dhi);
             g->loc_dlo = dlo; g->loc_dhi = dhi;
             if (!mix_ok) g->loc_KP = 0;
             for (int i = 0; i <= L.ncls; ++i) { g->loc_cls_q[i] = L.cls_q[i]; g->loc_cls_w[i] = L.cls_w[i]; }
@@ -613,6 +612,23 @@ int ldpc_debug_loc_layout(const int32_t *check_ptr, const int32_t *check_var, co
     return LDPC_OK;
 }
 
+int ldpc_debug_loc_variant(const int32_t *check_ptr, const int32_t *check_var, const int32_t *var_ptr,
+                           const int32_t *var_slot, int n, int m, int T, int32_t *variant) {
+    LDPC_REQUIRE(variant, "null variant");
+    LDPC_REQUIRE(T == 256 || T == 512 || T == 1024, "T must be 256, 512 or 1024");
+    HostGraph h;
+    int rc = host_graph_from_csr(check_ptr, check_var, var_ptr, var_slot, n, m, h);
+    if (rc) return rc;
+    LocLayout L;
+    L.T = T;
+    *variant = kLocNone;
+    if (!h.consistent || !build_loc_layout(h.n, h.m, h.cptr, h.cvar, h.vptr, h.vslot, L)) return LDPC_OK;
+    int dlo = 0, dhi = 0;
+    if (!loc_degree_range(L, dlo, dhi)) return LDPC_OK;
+    *variant = loc_variant(dlo, dhi, L.DVN, L.DVN0, L.DVN1, L.ABS0, L.ABS1, L.T, L.KP);
+    return LDPC_OK;
+}
+
 const char *ldpc_bp_kernel_name(const ldpc_graph *g, int early_stop) {
     return g ? bp_kernel_name(*g, early_stop) : "none";
 }
@@ -636,6 +652,7 @@ static int bec_host_locked(const ldpc_graph *g, uint8_t *words, int B, int max_i
     for (size_t i = 0; i < (size_t)B * n; ++i)
         LDPC_REQUIRE(words[i] <= 2, "channel word value outside {0, 1, 2}");
     Workspace &ws = workspace(nullptr);
+    std::lock_guard<std::mutex> wl(ws.mu);
     LDPC_HIP(ws.words.ensure((size_t)B * n));
     LDPC_HIP(ws.errors.ensure(sizeof(int32_t) * (size_t)B * (max_iters > 0 ? max_iters : 1)));
     LDPC_HIP(ws.itsb.ensure(sizeof(int32_t) * (size_t)B));
@@ -731,6 +748,7 @@ int ldpc_bp_decode_batch_dev(const ldpc_graph *g, const float *d_llr, int B, int
     if (sb) {
         std::lock_guard<std::mutex> lk(g_mu);
         Workspace &ws = workspace(stream);
+        std::lock_guard<std::mutex> wl(ws.mu);
         LDPC_HIP(ws.scratch.ensure(sb));
         scratch = static_cast<float *>(ws.scratch.p);
     }
@@ -753,6 +771,7 @@ int ldpc_bp_decode_batch(const int32_t *variable_to_check_list, const int32_t *c
     {
         std::lock_guard<std::mutex> lk(g_mu);
         Workspace &ws = workspace(nullptr);
+        std::lock_guard<std::mutex> wl(ws.mu);
         const size_t nb = (size_t)B * n;
         hipError_t e = ws.llr.ensure(nb * 4);
         if (e == hipSuccess) e = ws.post.ensure(nb * 4);
@@ -829,8 +848,8 @@ int ldpc_mc_batch_dev(const ldpc_graph *g, int channel, float param, uint64_t se
     }
     if (B == 0) return LDPC_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    std::lock_guard<std::mutex> lk(g_mu);
-    Workspace &ws = workspace(stream);
+    Workspace &ws = workspace(stream);  // this (device, stream)'s lock only: devices launch in parallel
+    std::lock_guard<std::mutex> wl(ws.mu);
     LDPC_HIP(ws.trial.ensure(sizeof(int32_t) * (size_t)B * (max_iters + 1)));
     LDPC_HIP(ws.its.ensure(sizeof(int32_t) * (size_t)B));
     LDPC_HIP(ws.cutoff.ensure(16));
@@ -879,6 +898,7 @@ int ldpc_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_gra
     const size_t E = (size_t)n * dv;
     std::lock_guard<std::mutex> lk(g_mu);
     Workspace &ws = workspace(nullptr);
+    std::lock_guard<std::mutex> wl(ws.mu);
     LDPC_HIP(ws.gchk.ensure(E * G * 4));
     LDPC_HIP(ws.gvar.ensure(E * G * 4));
     LDPC_HIP(ws.gatt.ensure((size_t)G * 4 + 4));
@@ -928,6 +948,7 @@ int ldpc_sample_csr_dev(int n, int m, const int32_t *var_ptr, const int32_t *che
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(g_mu);
     Workspace &ws = workspace(stream);
+    std::lock_guard<std::mutex> wl(ws.mu);
     int E = 0;
     const int32_t *vs, *cp, *vp;
     rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, stream, &E, &vs, &cp, &vp);
@@ -944,6 +965,7 @@ int ldpc_sample_csr(int n, int m, const int32_t *var_ptr, const int32_t *check_p
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(g_mu);
     Workspace &ws = workspace(nullptr);
+    std::lock_guard<std::mutex> wl(ws.mu);
     int E = 0;
     const int32_t *vs, *cp, *vp;
     rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, nullptr, &E, &vs, &cp, &vp);
@@ -976,8 +998,8 @@ int ldpc_mc_ensemble_batch_dev(int n, int dv, int dc, int channel, float param, 
     if (B == 0) return LDPC_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t E = (size_t)n * dv;
-    std::lock_guard<std::mutex> lk(g_mu);
-    Workspace &ws = workspace(stream);
+    Workspace &ws = workspace(stream);  // this (device, stream)'s lock only: devices launch in parallel
+    std::lock_guard<std::mutex> wl(ws.mu);
     LDPC_HIP(ws.gchk.ensure(E * B * 4));
     LDPC_HIP(ws.gvar.ensure(E * B * 4));
     LDPC_HIP(ws.trial.ensure(sizeof(int32_t) * (size_t)B * (max_iters + 1)));
@@ -1018,6 +1040,7 @@ int ldpc_ml_decode_batch(const ldpc_graph *g, const uint8_t *words, int B, uint8
     const size_t bytes = (size_t)B * g->n;
     std::lock_guard<std::mutex> lk(g_mu);
     Workspace &ws = workspace(nullptr);
+    std::lock_guard<std::mutex> wl(ws.mu);
     LDPC_HIP(ws.mlw.ensure(bytes));
     LDPC_HIP(ws.mlo.ensure(bytes));
     LDPC_HIP(ws.mlu.ensure(sizeof(int32_t) * (size_t)B));
@@ -1068,8 +1091,8 @@ int ldpc_mc_ml_batch_dev(const ldpc_graph *g, int n, int dv, int dc, float eps, 
     if (rc) return rc;
     if (B == 0) return LDPC_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    std::lock_guard<std::mutex> lk(g_mu);
-    Workspace &ws = workspace(stream);
+    Workspace &ws = workspace(stream);  // this (device, stream)'s lock only
+    std::lock_guard<std::mutex> wl(ws.mu);
     LDPC_HIP(ws.mlw.ensure((size_t)B * n));
     LDPC_HIP(ws.mlo.ensure((size_t)B * n));
     LDPC_HIP(ws.mlu.ensure(sizeof(int32_t) * (size_t)B));

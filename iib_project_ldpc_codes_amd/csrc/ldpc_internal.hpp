@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -60,6 +61,42 @@ struct LocLayout {
 };
 bool build_loc_layout(int n, int m, const std::vector<int32_t> &cptr, const std::vector<int32_t> &cvar,
                       const std::vector<int32_t> &vptr, const std::vector<int32_t> &vslot, LocLayout &L);
+
+// Check-degree range of a layout's classes (a mixed class counts its smaller check); false
+// when a mixed class is not (dhi - 1, dhi) -- the kernel pads a mixed pair's smaller check by
+// exactly one input.
+inline bool loc_degree_range(const LocLayout &L, int &dlo, int &dhi) {
+    dlo = 99;
+    dhi = 0;
+    for (int i = 0; i < L.ncls; ++i) {
+        dlo = std::min(dlo, L.cls_d[i] >> 8 ? L.cls_d[i] >> 8 : L.cls_d[i]);
+        dhi = std::max(dhi, L.cls_d[i] & 255);
+    }
+    bool ok = true;
+    for (int i = 0; i < L.ncls; ++i)
+        if (L.cls_d[i] >> 8) ok &= (L.cls_d[i] & 255) == dhi && (L.cls_d[i] >> 8) == dhi - 1;
+    return ok;
+}
+
+// The bp_loc_kernel instantiation family a local-edge layout runs on -- decided from the
+// WHOLE shape, never from the check degrees alone (a check-regular degree-6 graph with
+// variable degrees {2, 4} has loc_dlo == 6 but needs the RSU family's DVN = 3 rows):
+//   kLocReg36: <DLO=6, DHI=6, DVN0=2, DVN1=2, ABS0=ABS1=false> -- every check degree 6 and every
+//              variable degree 3 (the (3,6) codes); shapes T=256 KP 1-4, T=1024 KP 2-3, T=512 KP 5
+//   kLocRsu:   <DLO=5, DHI=6, DVN0=1, DVN1=3, ABS0=false, ABS1=true> -- check degrees 5..6, every
+//              slot-0 variable degree 2, slot-1 variables degree 2..4; T=256 KP 1-4, T=1024 KP 2-3,
+//              T=512 KP 8 / 10
+//   kLocNone:  no instantiation (the graph runs on bp_lds / bp_irr / bp_generic)
+enum LocVariant { kLocNone = 0, kLocReg36 = 1, kLocRsu = 2 };
+inline int loc_variant(int dlo, int dhi, int DVN, int dvn0, int dvn1, bool abs0, bool abs1, int T, int KP) {
+    if (KP <= 0) return kLocNone;
+    const bool reg36 = dlo == 6 && dhi == 6 && DVN == 2 && dvn0 == 2 && dvn1 == 2 && !abs0 && !abs1;
+    const bool rsu = !reg36 && dlo >= 5 && dhi == 6 && DVN == 3 && dvn0 == 1 && !abs0 && dvn1 <= 3;
+    const bool common = (T == 256 && KP >= 1 && KP <= 4) || (T == 1024 && KP >= 2 && KP <= 3);
+    if (reg36 && (common || (T == 512 && KP == 5))) return kLocReg36;
+    if (rsu && (common || (T == 512 && (KP == 8 || KP == 10)))) return kLocRsu;
+    return kLocNone;
+}
 
 // Irregular kernel (bp_irr_kernel): 1024 threads; LDS room for messages (bytes)
 // after the early-stop syndrome bits and the Monte-Carlo curve.

@@ -3243,18 +3243,15 @@ enum class BpPath { Loc, Lds36, Irr, Generic8, Generic16, Generic32, GenericG8, 
 #endif
 // bp_loc_kernel shapes: (check-degree range, non-local edges per variable, absent edges)
 // x (threads, check pairs per thread)
+int loc_variant_of(const ldpc_graph &g) {
+    return loc_variant(g.loc_dlo, g.loc_dhi, g.loc_DVN, g.loc_dvn0, g.loc_dvn1, g.loc_abs0, g.loc_abs1, g.loc_T,
+                       g.loc_KP);
+}
 bool loc_shape(const ldpc_graph &g, int &T, int &KP) {
-    if (!g.loc_KP) return false;
-    // (3,6): both slots 2 non-local edges, none absent; RSU-type rate-1/2 ensembles with
-    // variable degrees 2..4 and check degrees 5..6: slot 0 a degree-2 variable
-    const bool reg36 = g.loc_dlo == 6 && g.loc_dhi == 6 && g.loc_DVN == 2 && g.loc_dvn0 == 2 && g.loc_dvn1 == 2 &&
-                       !g.loc_abs0 && !g.loc_abs1;
-    const bool rsu = g.loc_dlo >= 5 && g.loc_dhi == 6 && g.loc_DVN == 3 && g.loc_dvn0 == 1 && !g.loc_abs0;
-    if (!reg36 && !rsu) return false;
+    if (loc_variant_of(g) == kLocNone) return false;
     T = g.loc_T;
     KP = g.loc_KP;
-    return (T == 256 && KP >= 1 && KP <= 4) || (T == 1024 && KP >= 2 && KP <= 3) ||
-           (T == 512 && (KP == 8 || KP == 10) && rsu) || (T == 512 && KP == 5 && reg36);
+    return true;
 }
 // messages | MC: per-iteration curve (16-byte padded) | min-sum MC: syndrome bits
 size_t loc_lds_bytes(const ldpc_graph &g, int iters = 0, bool mc = false, bool syn = false) {
@@ -3292,7 +3289,7 @@ BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc, int algo = 
     // on the other kernels, hard-decision-only ones run here; min-sum early stop: one check
     // class)
     const bool lds36_ms = LDPC_LDS36_MINSUM && algo == 1 && g.lane_var && g.dv == 3 && g.dc == 6 && g.loc_T != 512;
-    const bool one_cls = g.loc_dlo == 6 && g.loc_dhi == 6;
+    const bool one_cls = loc_variant_of(g) == kLocReg36;  // the one-class (3,6) instantiation
     const bool mode_ok = mc ? (algo == 0 || (LDPC_LOC_MSMC && one_cls))
                             : (!et || (LDPC_LOC_HARD_ET && hard_only && (algo == 0 || one_cls)));
     const bool mset = et && algo == 1;
@@ -3407,7 +3404,8 @@ hipError_t launch_loc(const ldpc_graph &g, BpArgs a, hipStream_t s) {
         a.loc_cls_w[i] = g.loc_cls_w[i];
     }
     for (int i = 0; i < 4; ++i) a.loc_cls_d[i] = g.loc_cls_d[i];
-    if (g.loc_dlo == 6) return launch_loc_deg<6, 6, 2, 2, false, false, ALGO, ET, MC>(g, a, T, KP, s);
+    // the template family from the whole layout shape (loc_variant), not the degrees alone
+    if (loc_variant_of(g) == kLocReg36) return launch_loc_deg<6, 6, 2, 2, false, false, ALGO, ET, MC>(g, a, T, KP, s);
     if constexpr (ET && ALGO == 1) return hipErrorInvalidValue;  // min-sum early stop: one check class only
     else return launch_loc_deg<5, 6, 1, 3, false, true, ALGO, ET, MC>(g, a, T, KP, s);
 }

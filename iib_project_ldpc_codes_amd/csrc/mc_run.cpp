@@ -9,7 +9,8 @@
 //
 // Here: device slot r of round R decodes trials [(R*ndev + r)*batch, +batch) with
 // the fused channel + decode + counter kernels (ldpc_mc_batch_dev /
-// ldpc_mc_ensemble_batch_dev) on its own stream; per round ONE ncclAllReduce
+// ldpc_mc_ensemble_batch_dev) on its own stream, launched from its own host thread;
+// per round ONE ncclAllReduce
 // (sum, int64) of [counter deltas | per-slot frame errors] over the devices
 // (RCCL, ncclCommInitAll; over xGMI on an MI355X node).  The stop rule is the
 // reference's `while frame_errors < stop and trials < num_tests` in global trial
@@ -17,7 +18,8 @@
 // crosses `stop` the slots before the crossing keep their batch, the crossing slot
 // re-runs its batch (Philox streams are keyed by trial index) with the in-batch
 // cut at its share, and later slots drop theirs.  Same trial partition and result
-// as montecarlo.MonteCarlo over W ranks.
+// as montecarlo.MonteCarlo over W ranks.  The accounting is mc_plan.hpp's, shared with the
+// host-only ldpc_debug_mc_plan (tested on the CPU for ndev = 1..8).
 //
 // RCCL is loaded at first use with dlopen(RTLD_LOCAL), so a process that also
 // holds torch's own RCCL copy keeps the two apart.
@@ -32,10 +34,12 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ldpc_internal.hpp"
 #include "ldpc_mi355x.h"
+#include "mc_plan.hpp"
 
 using namespace ldpc;
 
@@ -131,6 +135,93 @@ int launch_batch(const Run &r, Slot &s, uint64_t first_cw, int B, int64_t stop, 
                              r.early_stop, r.expurgation, stop, d_counters, s.stream);
 }
 
+// The devices' side of mc_drive (mc_plan.hpp).  One host thread per device launches that
+// device's batch (ldpc_mc_batch_dev takes only its (device, stream) workspace lock, so the
+// launches of different devices do not serialise); the per-round all-reduce is one RCCL
+// group call over the devices' communicators from the driving thread.
+struct DeviceBackend {
+    const Run &r;
+    std::vector<Slot> &slots;
+    const std::vector<ncclComm_t> &comms;
+    int C = 0, V = 0, ndev = 0;
+    std::vector<int64_t> G, red, tmp;
+
+    DeviceBackend(const Run &r_, std::vector<Slot> &s, const std::vector<ncclComm_t> &c, int C_)
+        : r(r_), slots(s), comms(c), C(C_), V(C_ + (int)s.size()), ndev((int)s.size()), G(C_, 0), red(V), tmp(V) {}
+    int64_t frames() const { return G[1]; }
+    int64_t trials() const { return G[0]; }
+    uint64_t first_cw(int64_t R, int i) const { return (uint64_t)(R * ndev + i) * (uint64_t)r.batch; }
+
+    // slot i: zeroed delta, its batch (no cut), its frame errors copied to position C + i
+    int launch_slot(int64_t R, int i, int B) {
+        Slot &s = slots[i];
+        RUN_HIP(hipSetDevice(s.dev));
+        RUN_HIP(hipMemsetAsync(s.d_send, 0, sizeof(int64_t) * V, s.stream));
+        int rc = launch_batch(r, s, first_cw(R, i), B, 0, s.d_send);
+        if (rc) return rc;
+        RUN_HIP(hipMemcpyAsync(s.d_send + C + i, s.d_send + 1, sizeof(int64_t), hipMemcpyDeviceToDevice, s.stream));
+        return LDPC_OK;
+    }
+    int round(int64_t R, const std::vector<int> &B, std::vector<int64_t> &f) {
+        std::vector<int> rcs(ndev, LDPC_OK);
+        std::vector<std::string> errs(ndev);
+        if (ndev == 1) {
+            rcs[0] = launch_slot(R, 0, B[0]);
+        } else {
+            std::vector<std::thread> th;
+            th.reserve(ndev);
+            for (int i = 0; i < ndev; ++i)
+                th.emplace_back([&, i]() {
+                    rcs[i] = launch_slot(R, i, B[i]);
+                    if (rcs[i]) errs[i] = ldpc_last_error();  // the error text is per thread
+                });
+            for (auto &t : th) t.join();
+        }
+        for (int i = 0; i < ndev; ++i)
+            if (rcs[i]) {
+                if (!errs[i].empty()) set_error(errs[i]);
+                return rcs[i];
+            }
+        RUN_NCCL(g_rccl.groupStart());
+        for (int i = 0; i < ndev; ++i) {
+            Slot &s = slots[i];
+            RUN_NCCL(g_rccl.allReduce(s.d_send, s.d_recv, (size_t)V, ncclInt64, ncclSum, comms[i], s.stream));
+        }
+        RUN_NCCL(g_rccl.groupEnd());
+        RUN_HIP(hipSetDevice(slots[0].dev));
+        RUN_HIP(hipMemcpyAsync(red.data(), slots[0].d_recv, sizeof(int64_t) * V, hipMemcpyDeviceToHost,
+                               slots[0].stream));
+        for (auto &s : slots) {
+            RUN_HIP(hipSetDevice(s.dev));
+            RUN_HIP(hipStreamSynchronize(s.stream));
+        }
+        for (int i = 0; i < ndev; ++i) f[i] = red[C + i];
+        return LDPC_OK;
+    }
+    int keep_round() {
+        for (int j = 0; j < C; ++j) G[j] += red[j];
+        return LDPC_OK;
+    }
+    int keep(int i) {  // slot i's own (un-reduced) delta
+        Slot &s = slots[i];
+        RUN_HIP(hipSetDevice(s.dev));
+        RUN_HIP(hipMemcpy(tmp.data(), s.d_send, sizeof(int64_t) * C, hipMemcpyDeviceToHost));
+        for (int j = 0; j < C; ++j) G[j] += tmp[j];
+        return LDPC_OK;
+    }
+    int cut(int64_t R, int i, int B, int64_t quota) {  // the same B trials, cut at the quota
+        Slot &s = slots[i];
+        RUN_HIP(hipSetDevice(s.dev));
+        RUN_HIP(hipMemsetAsync(s.d_tmp, 0, sizeof(int64_t) * V, s.stream));
+        int rc = launch_batch(r, s, first_cw(R, i), B, quota, s.d_tmp);
+        if (rc) return rc;
+        RUN_HIP(hipStreamSynchronize(s.stream));
+        RUN_HIP(hipMemcpy(tmp.data(), s.d_tmp, sizeof(int64_t) * C, hipMemcpyDeviceToHost));
+        for (int j = 0; j < C; ++j) G[j] += tmp[j];
+        return LDPC_OK;
+    }
+};
+
 int run_impl(const Run &r, int64_t num_tests, int64_t stop, double time_limit_s, const int *devices, int ndev,
              int64_t *counters, int64_t *rounds_out) {
     const int C = LDPC_MC_NCOUNT + r.max_iters + 1;
@@ -158,7 +249,6 @@ int run_impl(const Run &r, int64_t num_tests, int64_t stop, double time_limit_s,
         ctx.comms = comms;
         ctx.streams = streams;
     }
-    const std::vector<ncclComm_t> &comms = ctx.comms;
     std::vector<Slot> slots(ndev);
     auto cleanup = [&]() {
         for (auto &s : slots) {
@@ -190,80 +280,71 @@ int run_impl(const Run &r, int64_t num_tests, int64_t stop, double time_limit_s,
             if (rc) return rc;
         }
     }
-
-    std::vector<int64_t> G(C, 0), red(V), tmp(V);
-    const auto t0 = std::chrono::steady_clock::now();
+    McPlan P;
+    P.num_tests = num_tests;
+    P.stop = stop;
+    P.batch = r.batch;
+    P.ndev = ndev;
+    DeviceBackend be(r, slots, ctx.comms, C);
     int64_t rounds = 0;
-    auto frames = [&]() { return G[1]; };
-    auto trials = [&]() { return G[0]; };
-    auto slot_batch = [&](int i) -> int {
-        if (num_tests <= 0) return r.batch;
-        const int64_t left = num_tests - trials() - (int64_t)i * r.batch;
-        return (int)std::max<int64_t>(0, std::min<int64_t>(r.batch, left));
-    };
-    while (true) {
-        if (stop > 0 && frames() >= stop) break;
-        if (num_tests > 0 && trials() >= num_tests) break;
-        // 1. every slot decodes its batch into a zeroed delta (no cut), frame errors to slot C + i
-        for (int i = 0; i < ndev; ++i) {
-            Slot &s = slots[i];
-            RUN_HIP(hipSetDevice(s.dev));
-            RUN_HIP(hipMemsetAsync(s.d_send, 0, sizeof(int64_t) * V, s.stream));
-            rc = launch_batch(r, s, (uint64_t)(rounds * ndev + i) * r.batch, slot_batch(i), 0, s.d_send);
-            if (rc) return rc;
-            RUN_HIP(hipMemcpyAsync(s.d_send + C + i, s.d_send + 1, sizeof(int64_t), hipMemcpyDeviceToDevice,
-                                   s.stream));
-        }
-        // 2. one all-reduce over the devices
-        RUN_NCCL(g_rccl.groupStart());
-        for (int i = 0; i < ndev; ++i) {
-            Slot &s = slots[i];
-            RUN_NCCL(g_rccl.allReduce(s.d_send, s.d_recv, (size_t)V, ncclInt64, ncclSum, comms[i], s.stream));
-        }
-        RUN_NCCL(g_rccl.groupEnd());
-        RUN_HIP(hipSetDevice(slots[0].dev));
-        RUN_HIP(hipMemcpyAsync(red.data(), slots[0].d_recv, sizeof(int64_t) * V, hipMemcpyDeviceToHost,
-                               slots[0].stream));
-        for (auto &s : slots) {
-            RUN_HIP(hipSetDevice(s.dev));
-            RUN_HIP(hipStreamSynchronize(s.stream));
-        }
-        ++rounds;
-        int64_t round_frames = 0;
-        for (int i = 0; i < ndev; ++i) round_frames += red[C + i];
-        if (stop > 0 && frames() + round_frames >= stop) {
-            // 3. the crossing round: replay the sequential cut in trial order
-            int64_t before = frames();
-            for (int i = 0; i < ndev; ++i) {
-                const int64_t quota = stop - before;
-                if (quota <= 0) break;
-                Slot &s = slots[i];
-                RUN_HIP(hipSetDevice(s.dev));
-                const int64_t f = red[C + i];
-                if (quota > f) {  // whole batch kept
-                    RUN_HIP(hipMemcpy(tmp.data(), s.d_send, sizeof(int64_t) * C, hipMemcpyDeviceToHost));
-                } else {          // the crossing slot: cut at its share
-                    RUN_HIP(hipMemsetAsync(s.d_tmp, 0, sizeof(int64_t) * V, s.stream));
-                    rc = launch_batch(r, s, (uint64_t)((rounds - 1) * ndev + i) * r.batch, slot_batch(i), quota,
-                                      s.d_tmp);
-                    if (rc) return rc;
-                    RUN_HIP(hipStreamSynchronize(s.stream));
-                    RUN_HIP(hipMemcpy(tmp.data(), s.d_tmp, sizeof(int64_t) * C, hipMemcpyDeviceToHost));
-                }
-                for (int j = 0; j < C; ++j) G[j] += tmp[j];
-                before += tmp[1];
-            }
-            break;
-        }
-        for (int j = 0; j < C; ++j) G[j] += red[j];
-        if (time_limit_s > 0 &&
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > time_limit_s)
-            break;
-    }
-    std::memcpy(counters, G.data(), sizeof(int64_t) * C);
+    rc = mc_drive(P, be, time_limit_s, rounds);
+    if (rc) return rc;
+    std::memcpy(counters, be.G.data(), sizeof(int64_t) * C);
     if (rounds_out) *rounds_out = rounds;
     return LDPC_OK;
 }
+
+// Host-only stand-in for the devices (ldpc_debug_mc_plan): trial t is a frame error iff
+// fe[t] != 0; a batch counts its trials and frame errors, the cut keeps trials up to and
+// including the one that reaches the quota (mc_cutoff_kernel's rule).
+struct SeqBackend {
+    const uint8_t *fe = nullptr;
+    int64_t avail = 0;
+    int batch = 0, ndev = 0;
+    int64_t G[2] = {0, 0};
+    std::vector<int64_t> dt, df;  // the round's per-slot deltas
+    int64_t frames() const { return G[1]; }
+    int64_t trials() const { return G[0]; }
+    int count(int64_t first, int B, int64_t quota, int64_t &t, int64_t &f) const {
+        t = f = 0;
+        if (B > 0 && first + B > avail) {
+            set_error("ldpc_debug_mc_plan: the plan reads past the synthetic trial sequence");
+            return LDPC_EINVAL;
+        }
+        for (int j = 0; j < B; ++j) {
+            ++t;
+            f += fe[first + j] != 0;
+            if (quota > 0 && f >= quota) break;
+        }
+        return LDPC_OK;
+    }
+    int round(int64_t R, const std::vector<int> &B, std::vector<int64_t> &f) {
+        dt.assign(ndev, 0);
+        df.assign(ndev, 0);
+        for (int i = 0; i < ndev; ++i) {
+            int rc = count((R * ndev + i) * (int64_t)batch, B[i], 0, dt[i], df[i]);
+            if (rc) return rc;
+            f[i] = df[i];
+        }
+        return LDPC_OK;
+    }
+    int keep_round() {
+        for (int i = 0; i < ndev; ++i) keep(i);
+        return LDPC_OK;
+    }
+    int keep(int i) {
+        G[0] += dt[i];
+        G[1] += df[i];
+        return LDPC_OK;
+    }
+    int cut(int64_t R, int i, int B, int64_t quota) {
+        int64_t t = 0, f = 0;
+        int rc = count((R * ndev + i) * (int64_t)batch, B, quota, t, f);
+        G[0] += t;
+        G[1] += f;
+        return rc;
+    }
+};
 
 int check_common(int channel, int max_iters, int batch, const int *devices, int ndev, int64_t *counters) {
     if (!counters || !devices || ndev <= 0 || max_iters < 0 || batch <= 0) {
@@ -340,6 +421,30 @@ int ldpc_mc_run_csr(const int32_t *check_ptr, const int32_t *check_var, const in
     r.seed = seed; r.max_iters = max_iters; r.expurgation = expurgation; r.batch = batch;
     std::lock_guard<std::mutex> lk(g_run_mu);
     return run_impl(r, num_tests, stop_frame_errors, time_limit_s, devices, ndev, counters, rounds);
+}
+
+int ldpc_debug_mc_plan(const uint8_t *frame_error, int64_t num_trials, int64_t num_tests, int64_t stop_frame_errors,
+                       int batch, int ndev, int64_t *out) {
+    if (!out || (num_trials > 0 && !frame_error) || num_trials < 0 || batch <= 0 || ndev <= 0) {
+        set_error("ldpc_debug_mc_plan: need out[3], the trial sequence, batch > 0, ndev > 0");
+        return LDPC_EINVAL;
+    }
+    McPlan P;
+    P.num_tests = num_tests;
+    P.stop = stop_frame_errors;
+    P.batch = batch;
+    P.ndev = ndev;
+    SeqBackend be;
+    be.fe = frame_error;
+    be.avail = num_trials;
+    be.batch = batch;
+    be.ndev = ndev;
+    int64_t rounds = 0;
+    const int rc = mc_drive(P, be, 0.0, rounds);
+    out[0] = be.G[0];
+    out[1] = be.G[1];
+    out[2] = rounds;
+    return rc;
 }
 
 }  // extern "C"

@@ -48,10 +48,17 @@ def config(mc):
 
 
 def from_counters(mc, g):
-    """Snapshot dict from global counters g (numpy, BP counters then ML counters)."""
+    """Snapshot dict from global counters g (numpy, BP counters then ML counters).
+
+    The trial range ends at the first trial NOT counted.  The stop rule counts trials in
+    global trial order from the run's first trial (the in-batch cut, later ranks' dropped
+    batches, the num_tests clamp), so the counted trials are exactly [trial_base0,
+    trial_base0 + trials) -- which is next_trial() only when every round ran whole batches.
+    Resuming a stopped run with a higher stop then continues right after the cut."""
     nc = len(mc.counters)
+    _, trials = mc._frames_trials(g[:nc], g[nc:])
     return {"version": VERSION, "config": config(mc), "seed": int(mc.seed),
-            "trial_ranges": [[int(mc.trial_base0), int(mc.next_trial())]],
+            "trial_ranges": [[int(mc.trial_base0), int(mc.trial_base0) + int(trials)]],
             "counters": [int(x) for x in g[:nc]],
             "counters_ml": [int(x) for x in g[nc:]] if mc.optimal else None}
 

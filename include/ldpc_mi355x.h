@@ -315,6 +315,28 @@ int ldpc_debug_loc_layout(const int32_t *check_ptr, const int32_t *check_var, co
                           const int32_t *var_slot, int n, int m, int T, int32_t *shape, int32_t *var, int32_t *pos,
                           int32_t *info);
 
+/*
+ * Host-only: ldpc_mc_run's round accounting (csrc/mc_plan.hpp: per-slot batch clamp to
+ * num_tests, the crossing slot's cut at its share of the remaining frame errors, later slots
+ * dropped) driven by the same loop as the device run, on a synthetic trial sequence:
+ * trial t is a frame error iff frame_error[t] != 0 (t < num_trials).  out int64[3] = {trials,
+ * frame errors, rounds} -- equal to the sequential `while frame_errors < stop and trials <
+ * num_tests` loop (parallel_simulator.py:198) for every ndev.  LDPC_EINVAL if the plan would
+ * read past num_trials.
+ */
+int ldpc_debug_mc_plan(const uint8_t *frame_error, int64_t num_trials, int64_t num_tests, int64_t stop_frame_errors,
+                       int batch, int ndev, int64_t *out);
+
+/*
+ * Host-only: which bp_loc_kernel instantiation family the local-edge layout of this CSR
+ * graph (at T threads) would run on: 0 none (the graph takes another soft kernel), 1 the
+ * (3,6) family <6,6,2,2> (every check degree 6, every variable degree 3), 2 the RSU family
+ * <5,6,1,3> (check degrees 5..6, slot-0 variables degree 2, others 2..4).  Decided from the
+ * whole layout shape, exactly as the device dispatch decides it.
+ */
+int ldpc_debug_loc_variant(const int32_t *check_ptr, const int32_t *check_var, const int32_t *var_ptr,
+                           const int32_t *var_slot, int n, int m, int T, int32_t *variant);
+
 /* Name of the soft kernel a graph dispatches to (tests / bench); early_stop: 0 fixed count,
  * 1 early stop with posteriors, 2 early stop with hard decisions only (d_post == NULL). */
 const char *ldpc_bp_kernel_name(const ldpc_graph *g, int early_stop);

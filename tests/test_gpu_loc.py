@@ -147,3 +147,39 @@ def test_loc_mc_minsum_exact(torch, monkeypatch, kind, n, early_stop):
     want[3] = int(its.sum())
     assert 0 < want[1] < B  # both decoded and failed frames at this crossover probability
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("m", [1000, 10000])
+def test_loc_check6_var24_vs_oracle(torch, monkeypatch, m):
+    """Advisor round 2 (high): a check-regular degree-6 graph with variable degrees {2, 4}
+    has loc_dlo == 6 but DVN = 3; it must run on the RSU instantiation (its DVN = 3 gather
+    rows and absent-edge flags), not the (3,6) one.  SPA posteriors within tolerance and
+    min-sum bit-exact against the oracle, at the 256-thread (m = 1,000) and 512-thread
+    (m = 10,000) shapes; and the Monte-Carlo sum-product counters with early stop."""
+    from iib_project_ldpc_codes_amd import decoder
+    from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
+    from tests.graph_util import check6_var24
+    monkeypatch.delenv("LDPC_NO_LOC_LAYOUT", raising=False)
+    g = check6_var24(m, seed=5)
+    csr = [np.ascontiguousarray(a, np.int32) for a in g.to_csr()]
+    assert g.kernel_name() == "bp_loc_kernel"
+    llr = oracle.channel(oracle.CH_AWGN, 0.80, 5, 0, g.n, 32)
+    for iters in (1, 3, 5):
+        post, hard, its = decoder.bp_decode(g, llr, iters, "spa")
+        opost, ohard, _ = oracle.bp_decode_batch(csr, llr, iters, 0)
+        np.testing.assert_allclose(post, opost, rtol=SPA_RTOL, atol=SPA_ATOL)
+    post, hard, its = decoder.bp_decode(g, llr, 20, "minsum", alpha=0.75)
+    opost, ohard, _ = oracle.bp_decode_batch(csr, llr, 20, 1, alpha=0.75)
+    np.testing.assert_array_equal(post, opost)
+    np.testing.assert_array_equal(hard, ohard)
+    B, iters = 128, 20
+    mc = MonteCarlo(g, "awgn", 0.80, iters, algo="spa", early_stop=True, seed=3, batch=B)
+    mc.run_batch(0, B)
+    torch.cuda.synchronize()
+    got = mc.counters.cpu().numpy()
+    llr = oracle.channel(oracle.CH_AWGN, 0.80, 3, 0, g.n, B)
+    _, h, its = oracle.bp_decode_batch(csr, llr, iters, 0, early_stop=True)
+    fe, be = int(h.any(axis=1).sum()), int(h.sum())
+    assert got[0] == B and got[4] == int((llr < 0).sum())
+    assert abs(int(got[1]) - fe) <= 2, (got[:4], fe, be)
+    assert abs(int(got[3]) - int(its.sum())) <= 0.005 * its.sum() + 2, (got[:4], int(its.sum()))

@@ -97,3 +97,30 @@ def test_loc_layout_refuses_other_rates():
     rc = _native.lib().ldpc_debug_loc_layout(cptr.ctypes.data, cvar.ctypes.data, vptr.ctypes.data, vslot.ctypes.data,
                                              g.n, g.m, 256, shape.ctypes.data, None, None, None)
     assert rc == _native.LDPC_EUNSUP
+
+
+def loc_variant(g, T):
+    cptr, cvar, vptr, vslot = [np.ascontiguousarray(a, np.int32) for a in g.to_csr()]
+    out = np.zeros(1, np.int32)
+    rc = _native.lib().ldpc_debug_loc_variant(cptr.ctypes.data, cvar.ctypes.data, vptr.ctypes.data,
+                                              vslot.ctypes.data, g.n, g.m, T, out.ctypes.data)
+    assert rc == 0, _native.last_error()
+    return int(out[0])
+
+
+def test_loc_variant_from_whole_shape():
+    """The bp_loc_kernel family is chosen from the whole layout shape (advisor round 2): a
+    check-regular degree-6 graph with variable degrees {2, 4} (loc_dlo == 6, DVN = 3) must
+    take the RSU family (2), never the (3,6) family (1) whose rows hold DVN = 2 edges."""
+    from tests.graph_util import check6_var24
+    g = check6_var24(500, seed=3)
+    shape = layout(g, 256)[0]
+    assert shape[2] == 3 and (shape[22] & 255) == 1  # DVN 3, slot 0 = the degree-2 variables
+    assert all((d & 255) == 6 and not d >> 8 for d in shape[12:12 + shape[5]])  # every class degree 6
+    assert loc_variant(g, 256) == 2
+    g5 = check6_var24(5000, seed=4)
+    assert loc_variant(g5, 1024) == 2
+    assert loc_variant(g5, 512) == 0  # KP = 5 at T = 512: the RSU family has no such shape (another kernel runs)
+    assert loc_variant(TannerGraph.random_regular(1000, 3, 6, seed=2), 256) == 1
+    assert loc_variant(TannerGraph.random_regular(10000, 3, 6, seed=1), 512) == 1
+    assert loc_variant(ensembles.sample_irregular(ensembles.RSU_DL4, 2000, seed=21, deg2="zigzag"), 256) == 2

@@ -74,6 +74,27 @@ def test_checkpoint_resume_equals_uninterrupted(tmp_path):
     np.testing.assert_array_equal(snapshot.load(path)["counters"], want)
 
 
+def test_resume_after_frame_error_stop_continues_after_the_cut(tmp_path):
+    """Advisor round 2: a run stopped by the frame-error rule (in-batch cut) ends its trial
+    range at the first trial it did not count, so resuming it with a higher stop counts
+    exactly what one uninterrupted run to the higher stop counts (no skipped trials)."""
+    g = _graph()
+    mc = _mc(g)
+    first = oracle_batch_counters(g, 0, 64 * B, ITERS)
+    s1 = 5
+    mc.run(num_tests=0, stop_frame_errors=s1)
+    snap = mc.snapshot()
+    assert snap["counters"][1] == s1
+    assert snap["trial_ranges"][0][1] == snap["counters"][0] < mc.next_trial()  # cut inside a batch
+    mc2 = _mc(g)
+    mc2.restore(snap)
+    s2 = s1 + 7
+    res = mc2.run(num_tests=0, stop_frame_errors=s2)
+    want = oracle_batch_counters(g, 0, 64 * B, ITERS, remaining=s2)
+    np.testing.assert_array_equal(res["raw_counters"], want)
+    assert first[1] > s2  # the sequence holds enough frame errors for both stops
+
+
 def test_restore_rejects_other_configuration(tmp_path):
     g = _graph()
     mc = _mc(g)
