@@ -270,6 +270,20 @@ def onchip_rooflines(cw_iters_per_s, kernel):
             "issue_cycles_per_codeword_iteration": v_cyc,
             "wave_instr_per_codeword_iteration": d["wave_instr_per_codeword_iteration"],
             "cycles_per_wave_instr": d["cycles"]["valu"], "profile": rel, "profile_git": d.get("git")}
+    alg = algorithmic_valu_cycles()
+    valu["algorithmic"] = {"issue_cycles_per_codeword_iteration": alg["cycles"],
+                           "frac": alg["cycles"] * cw_iters_per_s / (SIMDS * CLOCK_HZ), "definition": alg["definition"]}
+    pmc = d.get("pmc_per_codeword_iteration", {})
+    prof_pmc = os.path.join(ROOT, "profiles", d.get("pmc_summary") or
+                            os.path.basename(ISSUE_PROFILE).replace("_issue_model.json", "_pmc_summary.json"))
+    if os.path.isfile(prof_pmc):  # VALU-active fraction of the profiled launch (PMC, not the model)
+        with open(prof_pmc) as f:
+            c = json.load(f)["counters"]
+        kernel_cycles = c["GRBM_GUI_ACTIVE"] / 8  # per XCD = the dispatch's shader-clock cycles
+        valu["pmc_valu_active_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / kernel_cycles
+        valu["pmc_profile"] = os.path.relpath(prof_pmc, ROOT)
+    elif pmc:
+        valu["pmc_valu_active_frac"] = None
     lds = {"bound": "lds", "achieved": l_cyc * cw_iters_per_s / 1e9, "peak": CUS * CLOCK_HZ / 1e9,
            "unit": "G LDS-cycles/s", "frac": l_cyc * cw_iters_per_s / (CUS * CLOCK_HZ),
            "lds_cycles_per_codeword_iteration": l_cyc,
@@ -277,6 +291,25 @@ def onchip_rooflines(cw_iters_per_s, kernel):
            "bank_conflict_cycles_per_codeword_iteration": d["lds_bank_conflict_cycles_per_codeword_iteration"],
            "cycles_per_wave_instr": d["cycles"]["lds"], "profile": rel, "profile_git": d.get("git")}
     return valu, lds
+
+
+def algorithmic_valu_cycles():
+    """The minimum VALU issue work of the headline decode per codeword-iteration in its chosen
+    formulation (no unpacks, clamps, sign handling, staging or loop control), SIMD-cycles at the
+    issue-model prices (packed f32 4, transcendental 8 per wave64 instruction):
+      check phase, per check pair (both degree-6 checks on float2, elementary-symmetric rule):
+        prefix (E, O) 4 x 2 packed ops, suffix 3 x (2 v_pk_mul + 4 v_pk_fma) + 4 for the last step
+        (its prefix set is {R_0}: no product), six output ratios 6 v_pk_mul + 12 v_rcp_f32
+        = 36 packed + 12 transcendental;
+      variable phase, per variable pair (degree 3: one local + two gathered ratios on float2):
+        R_j = E prod_{k != j} r_k by prefix / suffix products = 5 v_pk_mul.
+    For (3,6) n = 10,000: P = 2,500 check pairs, 5,000 variable pairs, 64 lanes per wave."""
+    P, VPAIRS = (N_BITS // 2) // 2, N_BITS // 2
+    check = (36 * 4 + 12 * 8) * P / 64
+    var = 5 * 4 * VPAIRS / 64
+    return {"cycles": check + var,
+            "definition": "check pair: 36 v_pk_* x4 + 12 v_rcp x8 cycles per 64 pairs; variable pair: 5 v_pk_mul x4 "
+                          "per 64 pairs; P=2500, 5000 variable pairs (bench.py algorithmic_valu_cycles)"}
 
 
 def load_traffic():

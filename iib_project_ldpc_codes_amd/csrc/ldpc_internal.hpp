@@ -46,7 +46,8 @@ struct ldpc_graph {
     int loc_cls_q[5] = {0}, loc_cls_d[4] = {0}, loc_cls_w[5] = {0};
     int32_t *loc_var = nullptr;   // [2*KP][2][T] variable id of var pair (thread, pair slot) half h, -1 pad
     int32_t *loc_pos = nullptr;   // [2*KP][DVN][T] non-local edge u's LDS words, h=0 | h=1 << 16
-    int32_t *loc_info = nullptr;  // [2*KP][T] bit u + 4h: edge u present; bits 8+2h: local edge index
+    int32_t *loc_info = nullptr;  // [2*KP][T] bit u + 4h: edge u present; bits 8+2h: local edge index jl;
+                                  // bit 16 + 4h + jl: the same one-hot (min-sum order masks)
 };
 
 // Local-edge layout (loc_layout.cpp): see the comment there.

@@ -683,6 +683,14 @@ template <int ALGO> struct Domain {
     static constexpr float in = ALGO == 0 ? 1.44269504088896341f : 1.0f;   // LLR -> message units
     static constexpr float out = ALGO == 0 ? 0.693147180559945309f : 1.0f; // message units -> LLR
 };
+// Channel LLR -> message.  Min-sum: l + 0 turns a -0 LLR into +0 (every other value is
+// unchanged), so no min-sum message is ever -0 (sums and differences of non-(-0) values
+// are not -0 in round-to-nearest) and the sign BIT of every check input equals the
+// oracle's (x < 0) -- which lets check_update_ms6 form signs with bit operations.
+template <int ALGO> __device__ __forceinline__ float to_msg(float l) {
+    if constexpr (ALGO == 0) return l * Domain<0>::in;
+    else return l + 0.0f;
+}
 
 // Sum-product check rule in ratio form, shared by all kernels and restated by
 // oracle check_update_spa: for an input message x (log2 units here) e = 2^-min(|x|, 23),
@@ -744,6 +752,47 @@ __device__ __forceinline__ float2 ratio_wire2(float2 R) {
                                  __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(R.y), 0x1p-23f, 1.0f));
     return lo - u;
 }
+
+#ifndef LDPC_MS_BITSIGN
+#define LDPC_MS_BITSIGN 1  // check_update_ms6: output signs by bit operations (see there)
+#endif
+// Inline-asm helpers (v_bitop3_b32, the VCC select, v_bfi_b32): the compiler's hazard
+// recognizer does not look inside inline asm, so their operands must not be fresh
+// transcendental (v_exp / v_log / v_rcp) results -- every use below takes LDS loads, min /
+// med3 / mul / bfe results or values from an earlier phase.
+// v_bitop3_b32 (gfx950) with truth table T over (S0, S1, S2) = (0xF0, 0xCC, 0xAA)
+template <int T>
+__device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "n"(T));
+    return r;
+}
+// a ^ b ^ c in one instruction (gfx950 has no v_xor3_b32: v_bitop3_b32 with table 0x96)
+__device__ __forceinline__ uint32_t xor3u(uint32_t a, uint32_t b, uint32_t c) { return bitop3<0x96>(a, b, c); }
+// |x| == m ? t : f as v_cmp (into VCC) + v_cndmask: the compiler would otherwise hold one
+// SGPR-pair mask per output of a check pair at once and spill SGPRs
+__device__ __forceinline__ uint32_t sel_abs_eq(float x, float m, uint32_t t, uint32_t f) {
+    uint32_t r;
+    asm("v_cmp_eq_f32_e64 vcc, |%1|, %2\n\tv_cndmask_b32 %0, %4, %3, vcc" : "=v"(r) : "v"(x), "v"(m), "v"(t), "v"(f) : "vcc");
+    return r;
+}
+// (m & a) | (~m & b): one v_bfi_b32
+__device__ __forceinline__ uint32_t bfi_u32(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t o;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(o) : "v"(m), "v"(a), "v"(b));
+    return o;
+}
+#ifndef LDPC_LOC_POST_LOGE
+#define LDPC_LOC_POST_LOGE 1  // bp_loc_kernel SPA posteriors: channel term log2(E) from registers
+#endif
+#ifndef LDPC_LOC_MS_BFI
+#define LDPC_LOC_MS_BFI 1  // bp_loc_kernel min-sum: ordered variable sums by bfe/bfi selects (ms_sum)
+#endif
+// (r & ~1) | (d & 1): one v_bfi_b32
+// (plain C: the compiler emits one v_and_or_b32 / v_bfi_b32 and, unlike for inline asm, inserts
+// the wait state gfx950 needs when an operand is a fresh transcendental result -- an asm
+// v_bfi_b32 right after the v_exp_f32 of the initial message read a stale register)
+__device__ __forceinline__ uint32_t bfi_lsb(uint32_t r, uint32_t d) { return (r & ~1u) | (d & 1u); }
 
 // a * b + c per lane as one v_pk_fma_f32 (the SLP vectoriser packs only some)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -837,6 +886,21 @@ __device__ __forceinline__ void check_update_ms6(float (&x)[6], float alpha) {
     // alpha*select(m2, m1), one multiply per edge instead of two per check
     asm volatile("" : "+v"(am1), "+v"(am2));
 #endif
+#if LDPC_MS_BITSIGN
+    // signs as bits (no input is -0, see to_msg, so the sign bit is the oracle's x < 0):
+    // S = XOR of the six sign bits, stamped onto both scaled minima once per check; each
+    // output is then the selected minimum XOR its own input's sign bit -- v_cmp, v_cndmask
+    // and one v_bitop3 / v_and + v_xor per output, no scalar mask arithmetic
+    const uint32_t S = xor3u(xor3u(__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2])),
+                             __float_as_uint(x[3]), __float_as_uint(x[4])) ^ __float_as_uint(x[5]);
+    const uint32_t M = 0x80000000u;
+    const uint32_t s1 = bitop3<0xF8>(__float_as_uint(am1), S, M), s2 = bitop3<0xF8>(__float_as_uint(am2), S, M);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const uint32_t mag = sel_abs_eq(x[i], m1, s2, s1);  // a | (b & M), then a ^ (b & M)
+        x[i] = __uint_as_float(bitop3<0x78>(mag, __float_as_uint(x[i]), M));
+    }
+#else
     bool neg = false;
 #pragma unroll
     for (int i = 0; i < 6; ++i) neg ^= (x[i] < 0.0f);
@@ -845,6 +909,7 @@ __device__ __forceinline__ void check_update_ms6(float (&x)[6], float alpha) {
         const float mag = ax[i] == m1 ? am2 : am1;
         x[i] = (neg ^ (x[i] < 0.0f)) ? -mag : mag;
     }
+#endif
 }
 
 
@@ -982,6 +1047,7 @@ struct BpArgs {
     const int32_t *loc_var, *loc_pos, *loc_info;
     int loc_P, loc_ncls, loc_words;
     int loc_cls_q[5], loc_cls_d[4], loc_cls_w[5];
+    uint32_t *work;  // bp_loc_kernel early stop with posteriors: next-codeword counter (zeroed per launch)
 };
 
 // ---------------------------------------------------------------------------
@@ -1056,12 +1122,12 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 #pragma unroll
             for (int k = 0; k < VPT; ++k) {
                 const int v = tid + k * T;
-                if (v < n) msg[v] = nx[k] * Domain<ALGO>::in;
+                if (v < n) msg[v] = to_msg<ALGO>(nx[k]);
             }
         } else {
             for (int v = tid; v < n; v += T) {
                 const float l = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
-                msg[v] = l * Domain<ALGO>::in;
+                msg[v] = to_msg<ALGO>(l);
                 err0 += (l < 0.0f);
             }
         }
@@ -1129,7 +1195,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             float l = __builtin_amdgcn_logf(L[i]);
             if (__builtin_expect(fabsf(l) >= 126.0f, 0)) {
                 const int vv = a.lane_var[tid + i * T];
-                l = vv >= 0 && !MC ? a.llr[(size_t)b * n + vv] * Domain<ALGO>::in : 0.0f;
+                l = vv >= 0 && !MC ? to_msg<ALGO>(a.llr[(size_t)b * n + vv]) : 0.0f;
             }
             return l;
         };
@@ -1435,9 +1501,26 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 //   neutral value (ratio 1 / sum 0) and write to a private dummy word.
 // ---------------------------------------------------------------------------
 // SGN (sum-product with early stop): every v->c ratio carries its variable's hard
-// decision in the sign bit; the pair's parities of those bits are the syndrome of the
-// previous variable phase (returned: 1 = a check of the pair unsatisfied), then the
-// magnitudes are the ratios.
+// decision in one bit; the pair's parities of those bits are the syndrome of the
+// previous variable phase (returned: 1 = a check of the pair unsatisfied).
+// LDPC_LOC_LSB: the bit is the ratio's mantissa LSB (a relative change of at most 2^-23,
+// far below the rule's ~10-ulp error), so the check rule takes the inputs as they are:
+// the parity is two v_xor3 chains and one OR per pair, and no input needs its sign
+// stripped.  Otherwise the sign bit, stripped before the rule.
+#ifndef LDPC_LOC_LSB
+#define LDPC_LOC_LSB 1
+#endif
+// XOR of the words of entries 0 .. N-1 (N <= D) of one half of x
+template <int N, int D>
+__device__ __forceinline__ uint32_t bits_parity(const float2 (&x)[D], bool hi) {
+    auto w = [&](int j) { return __float_as_uint(hi ? x[j].y : x[j].x); };
+    uint32_t p = w(0);
+    int j = 1;
+#pragma unroll
+    for (; j + 1 < N; j += 2) p = xor3u(p, w(j), w(j + 1));
+    if (j < N) p ^= w(j);
+    return p;
+}
 template <int D, int ALGO, bool MIXED = false, bool SGN = false>
 __device__ __forceinline__ int loc_check_pair(float *msg, int W, int Nc, int i, float2 &l0, float2 &l1, float alpha) {
     constexpr int U = D - 2;
@@ -1452,7 +1535,11 @@ __device__ __forceinline__ int loc_check_pair(float *msg, int W, int Nc, int i, 
     }
     if constexpr (U % 2) x[D - 1] = *reinterpret_cast<const float2 *>(msg + W + (U / 2) * 4 * Nc + 2 * i);
     int unsat = 0;
-    if constexpr (SGN) {
+    if constexpr (SGN && LDPC_LOC_LSB) {  // raw parity words: the caller ORs them and tests bit 0 once
+        // a mixed pair's .x check has D - 1 inputs: its pad slot holds the rule's output for the
+        // padding input (an arbitrary LSB), not a variable's decision
+        unsat = (int)(bits_parity<MIXED ? D - 1 : D, D>(x, false) | bits_parity<D, D>(x, true));
+    } else if constexpr (SGN) {
         uint32_t px = 0, py = 0;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
@@ -1518,6 +1605,22 @@ __device__ __forceinline__ V ld_fresh(const V *p, int idx) {
     return p[idx];
 }
 
+// Workgroup-wide OR of a per-lane predicate with ONE barrier (__syncthreads_or reduces
+// through a wave DPP chain, an LDS atomic and three barriers): each wave whose ballot is
+// non-zero has lane 0 store 1 to flag[par]; after the barrier every thread reads it; thread 0
+// then clears flag[par ^ 1] -- its previous readers are all past this barrier, and its next
+// writers are behind the next one.  flag[] must be zero before the first call; alternate par.
+__device__ __forceinline__ bool block_any(int pred, uint32_t *flag, int par) {
+    if (__builtin_amdgcn_ballot_w64(pred != 0) != 0 && (threadIdx.x & (kWave - 1)) == 0) flag[par] = 1u;
+    __syncthreads();
+    const bool any = flag[par] != 0u;
+    if (threadIdx.x == 0) flag[par ^ 1] = 0u;
+    return any;
+}
+#ifndef LDPC_LOC_BLOCK_ANY
+#define LDPC_LOC_BLOCK_ANY 1  // bp_loc_kernel early stop: block_any (one barrier) for the stop test
+#endif
+
 template <int N> using int_c = std::integral_constant<int, N>;
 template <bool B> using bool_c = std::integral_constant<bool, B>;
 
@@ -1543,11 +1646,13 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     // variable's decision XORs its checks' bits of an LDS syndrome (a few atomics once
     // decoding settles) and the next check phase tests that syndrome
     constexpr bool MSET = ET && ALGO == 1;
+    constexpr bool SGN_LSB = ET && ALGO == 0 && LDPC_LOC_LSB;
     constexpr int VP = 2 * KP;  // variable pairs per thread
     constexpr int DVM = DVN0 > DVN1 ? DVN0 : DVN1;
     constexpr int DVA = DVM > 0 ? DVM : 1;
     constexpr int DVP = DVA;  // rows of loc_pos per var pair
     extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ uint32_t stop_flag[2];  // early stop: block_any's double-buffered flag
     float *msg = reinterpret_cast<float *>(smem);
     const int tid = threadIdx.x;
     const int n = a.n, iters = a.max_iters;
@@ -1595,6 +1700,25 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     // the local one spliced in at its index jl (the oracle's order: bit-exact)
     auto ms_sum = [&](auto dn_tag, int v, const float2 &Lv, const float2 &lv, const float2 (&cv)[DVA]) {
         constexpr int DN = decltype(dn_tag)::value;
+        if constexpr (DN == 2 && LDPC_LOC_MS_BFI) {
+            // three terms in order: jl = 0 (ml, n0, n1), 1 (n0, ml, n1), 2 (n0, n1, ml); the masks
+            // jl == 0 / jl == 2 are sign-extended one-hot bits of loc_info (v_bfe_i32), the
+            // selects v_bfi_b32 -- VALU only, no per-lane masks held in SGPRs
+            float s2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t e0 = (uint32_t)__builtin_amdgcn_sbfe((int)inf[v], 16 + 4 * h, 1);
+                const uint32_t e2 = (uint32_t)__builtin_amdgcn_sbfe((int)inf[v], 18 + 4 * h, 1);
+                const uint32_t ml = __float_as_uint(h ? lv.y : lv.x);
+                const uint32_t n0 = __float_as_uint(h ? cv[0].y : cv[0].x), n1 = __float_as_uint(h ? cv[1].y : cv[1].x);
+                const float a0 = __uint_as_float(bfi_u32(e0, ml, n0));
+                const uint32_t u = bfi_u32(e0, n0, ml);
+                const float a1 = __uint_as_float(bfi_u32(e2, n1, u));
+                const float a2 = __uint_as_float(bfi_u32(e2, ml, n1));
+                s2[h] = (((h ? Lv.y : Lv.x) + a0) + a1) + a2;
+            }
+            return make_float2(s2[0], s2[1]);
+        }
         float s2[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1642,9 +1766,23 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             }
         }
     };
-    for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    // EP (early stop, posteriors asked for): a persistent grid takes codewords from a global
+    // counter (frames stop at different iterations) and keeps each variable pair's product of
+    // incoming c->v ratios (min-sum: its posterior sum) of the latest variable phase in the
+    // workgroup's slab, a.scratch + blockIdx.x * VP * T float2 (lane-contiguous stores, L2-
+    // resident: 40 KB per workgroup); the stopping iteration's posteriors come from there.
+    const bool ep = ET && !MC && a.post != nullptr;
+    float2 *slab = ep ? reinterpret_cast<float2 *>(a.scratch) + (size_t)blockIdx.x * VP * T : nullptr;
+    __shared__ int next_b;
+    for (int round = 0;; ++round) {
+        if (ep && tid == 0) next_b = (int)atomicAdd(a.work, 1u);
+        __syncthreads();  // the previous codeword's outputs are out of LDS; next_b visible
+        const int b = ep ? __builtin_amdgcn_readfirstlane(next_b) : (int)blockIdx.x + round * (int)gridDim.x;
+        if (b >= a.B) break;
         const uint64_t cw = a.first_cw + (uint64_t)b;
-        __syncthreads();  // the previous codeword's outputs are out of LDS
+        if constexpr (ET) {
+            if (tid == 0) stop_flag[0] = stop_flag[1] = 0u;  // visible after the staging barrier
+        }
         int err0 = 0;
         if constexpr (MC) {
             for (int i = tid; i <= iters; i += T) curve[i] = 0;
@@ -1652,13 +1790,13 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                 for (int i = tid; i < nsw; i += T) syn[i] = 0u;
             for (int v = tid; v < n; v += T) {
                 const float l = chan_soft(a.ch, cw, v);
-                msg[v] = l * Domain<ALGO>::in;
+                msg[v] = to_msg<ALGO>(l);
                 err0 += (l < 0.0f);
             }
         } else {
             if constexpr (MSET)
                 for (int i = tid; i < nsw; i += T) syn[i] = 0u;
-            for (int v = tid; v < n; v += T) msg[v] = a.llr[(size_t)b * n + v] * Domain<ALGO>::in;
+            for (int v = tid; v < n; v += T) msg[v] = to_msg<ALGO>(a.llr[(size_t)b * n + v]);
         }
         __syncthreads();
         if constexpr (MC) {
@@ -1686,7 +1824,11 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             if constexpr (SPA) {
                 w = make_float2(__builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].x, -23.0f, 23.0f)),
                                 __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].y, -23.0f, 23.0f)));
-                if constexpr (ET) w = make_float2(copysignf(w.x, L[v].x), copysignf(w.y, L[v].y));
+                if constexpr (ET && LDPC_LOC_LSB)  // the channel decision in the LSB
+                    w = make_float2(__uint_as_float(bfi_lsb(__float_as_uint(w.x), (uint32_t)(L[v].x < 0.0f))),
+                                    __uint_as_float(bfi_lsb(__float_as_uint(w.y), (uint32_t)(L[v].y < 0.0f))));
+                else if constexpr (ET)
+                    w = make_float2(copysignf(w.x, L[v].x), copysignf(w.y, L[v].y));
                 L[v] = make_float2(__builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].x, -126.0f, 126.0f)),
                                    __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].y, -126.0f, 126.0f)));
             } else {
@@ -1736,12 +1878,15 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                     const float2 P = DN > 0 ? pre[DV - 1] * cv[DN > 0 ? DN - 1 : 0] : pre[DV - 1];
                     dec = (int)(P.x < 1.0f) | ((int)(P.y < 1.0f) << 1);
                     if constexpr (ET) {
-                        sx = (uint32_t)(dec & 1) << 31;
-                        sy = (uint32_t)(dec >> 1) << 31;
+                        sx = LDPC_LOC_LSB ? (uint32_t)(dec & 1) : (uint32_t)(dec & 1) << 31;
+                        sy = LDPC_LOC_LSB ? (uint32_t)(dec >> 1) : (uint32_t)(dec >> 1) << 31;
                     }
                     if constexpr (ET && !MC) hbits = (hbits & ~((HB)3 << (2 * v))) | ((HB)dec << (2 * v));
                 }
                 auto sgn = [&](float2 R) {
+                    if constexpr (ET && LDPC_LOC_LSB)  // LSB := decision (one v_bfi_b32 per value)
+                        return make_float2(__uint_as_float(bfi_lsb(__float_as_uint(R.x), sx)),
+                                           __uint_as_float(bfi_lsb(__float_as_uint(R.y), sy)));
                     if constexpr (ET) return make_float2(__uint_as_float(__float_as_uint(R.x) | sx),
                                                          __uint_as_float(__float_as_uint(R.y) | sy));
                     return R;
@@ -1754,9 +1899,11 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                     at(a1[j - 1]) = R.y;
                     if (j < DV - 1) suf = suf * cv[j - 1];
                 }
+                if (ep) slab[v * T + tid] = loc[v] * suf;  // prod of the incoming c->v ratios
                 loc[v] = sgn(ratio_wire2(DN > 0 ? L[v] * suf : L[v]));
             } else {
                 const float2 s = ms_sum(dn_tag, v, L[v], loc[v], cv);
+                if (ep) slab[v * T + tid] = s;  // the posterior itself
 #pragma unroll
                 for (int u = 0; u < DN; ++u) {
                     at(a0[u]) = s.x - cv[u].x;
@@ -1784,6 +1931,10 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                 for (int v = 0; v < VP; ++v)
 #pragma unroll
                     for (int u = 0; u < DVA; ++u) asm volatile("" : "+v"(sp[v][u]));
+            }
+            if constexpr (ALGO == 1) {  // the order masks (ms_sum) are re-derived per iteration, not held
+#pragma unroll
+                for (int v = 0; v < VP; ++v) asm volatile("" : "+v"(inf[v]));
             }
             // ---- check phase ----
 #pragma unroll
@@ -1818,7 +1969,10 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             if constexpr (ET) {
                 // the syndrome of the previous variable phase's decisions: stop when every
                 // check is satisfied (oracle: after that iteration)
-                if (!__syncthreads_or(unsat | (it == 0))) {
+                if constexpr (SGN_LSB) unsat &= 1;  // the parities are in bit 0 of the OR of the pairs' words
+                const bool more = LDPC_LOC_BLOCK_ANY ? block_any(unsat | (it == 0), stop_flag, it & 1)
+                                                     : __syncthreads_or(unsat | (it == 0));
+                if (!more) {
                     stopped = true;
                     break;
                 }
@@ -1851,6 +2005,48 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             if (tid == 0) a.its[b] = it;
             continue;
         }
+        if constexpr (ET && !MC) {
+            if (stopped && ep) {
+                // posteriors of the stopping iteration from the slab (its last variable phase):
+                // SPA log2 E + log2(prod c->v) -- the oracle's L + sum of the c->v messages -- and
+                // the decisions that satisfied every check (hbits) as the hard decisions; staged
+                // through LDS (posteriors in words [0, n), decision bytes after them: the messages
+                // are dead once the stop is known)
+                uint8_t *hb = reinterpret_cast<uint8_t *>(msg + n);
+#pragma unroll
+                for (int v = 0; v < VP; ++v) {
+                    const float2 q = slab[v * T + tid];
+                    float2 pv;
+                    if constexpr (SPA) {
+                        pv = make_float2(__builtin_amdgcn_logf(L[v].x) + __builtin_amdgcn_logf(q.x),
+                                         __builtin_amdgcn_logf(L[v].y) + __builtin_amdgcn_logf(q.y));
+                    } else {
+                        pv = q;
+                    }
+                    const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid), v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
+                    if constexpr (SPA) {  // a clamped E (|LLR| > 87 nats): the channel value itself
+                        const float lx = __builtin_amdgcn_logf(L[v].x), ly = __builtin_amdgcn_logf(L[v].y);
+                        if (v0 >= 0 && fabsf(lx) >= 125.5f) pv.x = to_msg<ALGO>(a.llr[(size_t)b * n + v0]) + __builtin_amdgcn_logf(q.x);
+                        if (v1 >= 0 && fabsf(ly) >= 125.5f) pv.y = to_msg<ALGO>(a.llr[(size_t)b * n + v1]) + __builtin_amdgcn_logf(q.y);
+                    }
+                    if (v0 >= 0) {
+                        msg[v0] = pv.x;
+                        hb[v0] = (uint8_t)((hbits >> (2 * v)) & 1);
+                    }
+                    if (v1 >= 0) {
+                        msg[v1] = pv.y;
+                        hb[v1] = (uint8_t)((hbits >> (2 * v + 1)) & 1);
+                    }
+                }
+                __syncthreads();
+                for (int v = tid; v < n; v += T) {
+                    a.post[(size_t)b * n + v] = msg[v] * Domain<ALGO>::out;
+                    if (a.hard) a.hard[(size_t)b * n + v] = hb[v];
+                }
+                if (a.its && tid == 0) a.its[b] = it;
+                continue;
+            }
+        }
         if constexpr (ET) {
             if (stopped) {  // hard decisions of the stopping iteration (no posteriors asked for)
 #pragma unroll
@@ -1877,10 +2073,25 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             for (int u = 0; u < DN; ++u) spv[u] = load_sp(v, u);
             gather(dn_tag, abs_tag, v, spv, cv, a0, a1);
             if constexpr (SPA) {
-                const float *lb = a.llr + (size_t)b * n;
-                const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid), v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
-                float2 s = make_float2(v0 >= 0 ? ld_fresh(lb, v0) * Domain<ALGO>::in : 0.0f,
-                                       v1 >= 0 ? ld_fresh(lb, v1) * Domain<ALGO>::in : 0.0f);
+                float2 s;
+                if constexpr (LDPC_LOC_POST_LOGE) {
+                    // the channel term from the register-held E = 2^L: log2 E is L to ~1e-7 (no
+                    // second 40 KB read of the codeword's LLRs); a clamped E (|LLR| > 87 nats) takes
+                    // the input value itself
+                    s = make_float2(__builtin_amdgcn_logf(L[v].x), __builtin_amdgcn_logf(L[v].y));
+                    if (fabsf(s.x) >= 125.5f || fabsf(s.y) >= 125.5f) {
+                        const float *lb = a.llr + (size_t)b * n;
+                        const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid);
+                        const int v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
+                        if (fabsf(s.x) >= 125.5f && v0 >= 0) s.x = to_msg<ALGO>(lb[v0]);
+                        if (fabsf(s.y) >= 125.5f && v1 >= 0) s.y = to_msg<ALGO>(lb[v1]);
+                    }
+                } else {
+                    const float *lb = a.llr + (size_t)b * n;
+                    const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid), v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
+                    s = make_float2(v0 >= 0 ? to_msg<ALGO>(ld_fresh(lb, v0)) : 0.0f,
+                                    v1 >= 0 ? to_msg<ALGO>(ld_fresh(lb, v1)) : 0.0f);
+                }
                 s = s + make_float2(__builtin_amdgcn_logf(loc[v].x), __builtin_amdgcn_logf(loc[v].y));
 #pragma unroll
                 for (int u = 0; u < DN; ++u)
@@ -1976,7 +2187,7 @@ __global__ __launch_bounds__(T) void bp_generic_kernel(BpArgs a) {
         int err0 = 0;
         for (int v = tid; v < n; v += T) {
             const float l = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
-            const float l2 = l * Domain<ALGO>::in;
+            const float l2 = to_msg<ALGO>(l);
             Ls[v] = l2;
             err0 += (l < 0.0f);
             for (int e = a.vptr[v]; e < a.vptr[v + 1]; ++e) ST(a.vslot[e], l2);
@@ -2169,7 +2380,7 @@ __global__ __launch_bounds__(kIrrT) void bp_irr_kernel(BpArgs a) {
             float l = 0.0f;
             if (v >= 0) l = MC ? chan_soft(a.ch, cw, v) : a.llr[(size_t)b * n + v];
             err0 += (v >= 0) & (l < 0.0f);
-            L[i] = l * Domain<ALGO>::in;
+            L[i] = to_msg<ALGO>(l);
             const float w = v2c_rwire<ALGO>(L[i]);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -3241,8 +3452,27 @@ enum class BpPath { Loc, Lds36, Irr, Generic8, Generic16, Generic32, GenericG8, 
 #ifndef LDPC_LOC_HARD_ET
 #define LDPC_LOC_HARD_ET 1  // early-stop decodes without posteriors on bp_loc_kernel
 #endif
+#ifndef LDPC_LOC_ET_POST
+#define LDPC_LOC_ET_POST 1  // early-stop decodes with posteriors on bp_loc_kernel (slab, persistent grid)
+#endif
 // bp_loc_kernel shapes: (check-degree range, non-local edges per variable, absent edges)
 // x (threads, check pairs per thread)
+// Early stop with posteriors on bp_loc_kernel: persistent workgroups (two per CU, the most
+// any bp_loc_kernel shape keeps resident), each with a VP x T float2 slab in scratch.
+int loc_ep_grid() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return 2 * cus;
+}
+size_t loc_ep_slab_floats(const ldpc_graph &g) {
+    return (size_t)loc_ep_grid() * (size_t)(2 * g.loc_KP) * (size_t)g.loc_T * 2;
+}
+
 int loc_variant_of(const ldpc_graph &g) {
     return loc_variant(g.loc_dlo, g.loc_dhi, g.loc_DVN, g.loc_dvn0, g.loc_dvn1, g.loc_abs0, g.loc_abs1, g.loc_T,
                        g.loc_KP);
@@ -3290,8 +3520,10 @@ BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc, int algo = 
     // class)
     const bool lds36_ms = LDPC_LDS36_MINSUM && algo == 1 && g.lane_var && g.dv == 3 && g.dc == 6 && g.loc_T != 512;
     const bool one_cls = loc_variant_of(g) == kLocReg36;  // the one-class (3,6) instantiation
+    // early stop with posteriors stages n posteriors + n decision bytes in the message LDS
+    const bool ep_ok = LDPC_LOC_ET_POST && (size_t)std::max(g.loc_words + 64, g.n) * 4 >= (size_t)g.n * 5;
     const bool mode_ok = mc ? (algo == 0 || (LDPC_LOC_MSMC && one_cls))
-                            : (!et || (LDPC_LOC_HARD_ET && hard_only && (algo == 0 || one_cls)));
+                            : (!et || (LDPC_LOC_HARD_ET && (hard_only || ep_ok) && (algo == 0 || one_cls)));
     const bool mset = et && algo == 1;
     if (LDPC_LOC && mode_ok && iters > 0 && !lds36_ms && loc_shape(g, lT, lKP) &&
         loc_lds_bytes(g, iters, mc || mset, mset) <= kLdsMax - 2048)
@@ -3365,12 +3597,20 @@ hipError_t launch_generic(const ldpc_graph &g, BpArgs a, hipStream_t s) {
 }
 
 template <int DLO, int DHI, int D0, int D1, bool A0, bool A1, int T, int KP, int ALGO, bool ET, bool MC>
-hipError_t launch_loc_shape(const ldpc_graph &g, const BpArgs &a, hipStream_t s) {
+hipError_t launch_loc_shape(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     auto k = bp_loc_kernel<DLO, DHI, D0, D1, KP, T, ALGO, A0, A1, ET, MC>;
     const size_t lds = loc_lds_bytes(g, a.max_iters, MC || (ET && ALGO == 1), ET && ALGO == 1);
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3(a.B), dim3(T), lds, s, a);
+    unsigned grid = (unsigned)a.B;
+    if (ET && !MC && a.post) {  // early stop with posteriors: persistent grid, slab + counter in scratch
+        if (!a.scratch) return hipErrorInvalidValue;
+        grid = (unsigned)std::min<int>(a.B, loc_ep_grid());
+        a.work = reinterpret_cast<uint32_t *>(a.scratch + loc_ep_slab_floats(g));
+        e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, s, a);
     return hipGetLastError();
 }
 
@@ -3507,7 +3747,9 @@ size_t bp_scratch_bytes(const ldpc_graph &g, int B) {
     const size_t irr = g.irr_lane && irr_slab(g) ? (size_t)g.irr_P * 4 * (size_t)grid : 0;
     const size_t per = ((size_t)g.E * 5 + (size_t)g.n * 4 + 15) & ~(size_t)15;
     const size_t gen = generic_lds_bytes(g, 0, true) + 4096 <= kLdsMax ? 0 : per * (size_t)grid;
-    return std::max(irr, gen);
+    // bp_loc_kernel early stop with posteriors: per-workgroup slabs + the codeword counter
+    const size_t loc = g.loc_KP ? loc_ep_slab_floats(g) * 4 + 64 : 0;
+    return std::max(std::max(irr, gen), loc);
 }
 
 const char *bp_kernel_name(const ldpc_graph &g, int early_stop) {

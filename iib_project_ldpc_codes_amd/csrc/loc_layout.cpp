@@ -450,6 +450,7 @@ bool build_loc_layout(int n, int m, const std::vector<int32_t> &cptr, const std:
                                  (uint32_t)((((vi * DVN + uu) * 2 + h) * 64 + (t & 63)) % L.words) << (16 * h);
 #endif
                     info |= (uint32_t)jl << (8 + 2 * h);
+                    if (v >= 0 && jl < 4) info |= 1u << (16 + 4 * h + jl);  // one-hot copy (min-sum masks)
                 }
                 for (int u = 0; u < DVN; ++u) L.pos[((size_t)vi * DVN + u) * T + t] = (int32_t)pk[u];
                 L.info[(size_t)vi * T + t] = (int32_t)info;

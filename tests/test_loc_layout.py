@@ -56,6 +56,7 @@ def check_invariants(g, T):
                 assert bin((bits >> (4 * h)) & 15).count("1") == deg - 1
                 jl = (bits >> (8 + 2 * h)) & 3
                 assert 0 <= jl < deg
+                assert (bits >> (16 + 4 * h)) & 15 == 1 << jl  # one-hot copy of jl
                 for u in range(DVN):
                     w = (pos[vi, u, t] >> (16 * h)) & 0xFFFF
                     if u < deg - 1:
