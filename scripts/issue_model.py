@@ -51,14 +51,27 @@ KERNELS = {
             "bp_loc_kernel<6,6,2,2,KP=5,T=512,SPA,fixed-count>", 512, 5),
     "loc1024": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi3ELi1024ELi0ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
                 "bp_loc_kernel<6,6,2,2,KP=3,T=1024,SPA,fixed-count>", 1024, 3),
+    "loc_et": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi5ELi512ELi0ELb0ELb0ELb1ELb0EEEvNS0_6BpArgsE",
+               "bp_loc_kernel<6,6,2,2,KP=5,T=512,SPA,early-stop>", 512, 5),
+    "loc_ms": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi5ELi512ELi1ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
+               "bp_loc_kernel<6,6,2,2,KP=5,T=512,min-sum,fixed-count>", 512, 5),
     "lds36": ("_ZN4ldpc12_GLOBAL__N_113bp_lds_kernelILi3ELi6ELi1024ELi10ELi0ELb0ELb0EEEvNS0_6BpArgsE",
               "bp_lds_kernel<3,6,1024,10,SPA,fixed-count>", 1024, None),
 }
 
 
-def loc_parts(bb, T, KP):
+def loc_parts(bb, T, KP, stats=None):
+    """stats (scripts/diag/decode_launch.py output): early-stop launches -- per codeword-iteration
+    the check blocks run check_phases / sum_its times, the variable block variable_phases /
+    sum_its, the per-codeword blocks batch / sum_its (fixed count: 1, (ITERS-1)/ITERS, 1/ITERS)."""
     P = (N * DV // DC) // 2
     waves = T // 64
+    if stats:
+        r_chk = stats["check_phases"] / stats["sum_its"]
+        r_var = stats["variable_phases"] / stats["sum_its"]
+        r_cw = stats["batch"] / stats["sum_its"]
+    else:
+        r_chk, r_var, r_cw = 1.0, (ITERS - 1) / ITERS, 1.0 / ITERS
     chk = [i for i, (_, ins) in enumerate(bb) if ins.count("ds_read_b128") == 2 and ins.count("ds_write_b128") == 2]
     assert len(chk) == KP, len(chk)
     var = max(range(len(bb)), key=lambda i: bb[i][1].count("ds_read_b32"))
@@ -66,13 +79,13 @@ def loc_parts(bb, T, KP):
     execs = {}
     for k, i in enumerate(chk):
         lanes = min(max(P - k * T, 0), T)
-        execs[i] = (lanes + 63) // 64
-    execs[var] = waves * (ITERS - 1) / ITERS
+        execs[i] = (lanes + 63) // 64 * r_chk
+    execs[var] = waves * r_var
     parts = []
     for i, (_, ins) in enumerate(bb):
-        parts.append((ins, execs.get(i, waves / ITERS)))
+        parts.append((ins, execs.get(i, waves * r_cw)))
     return parts, {"check_slot_waves": [execs[i] for i in chk], "variable": execs[var],
-                   "other_blocks": waves / ITERS}
+                   "other_blocks": waves * r_cw}
 
 
 def lds36_parts(bb, T):
@@ -95,6 +108,11 @@ def main():
     if "--kernel" in sys.argv:
         kind = sys.argv[sys.argv.index("--kernel") + 1]
         argv.remove(kind)
+    stats = None
+    if "--stats" in sys.argv:  # an early-stop launch: its iteration statistics
+        sp = sys.argv[sys.argv.index("--stats") + 1]
+        argv.remove(sp)
+        stats = json.load(open(sp))
     src, pmc_path, out_path = argv[:3]
     sha = argv[3] if len(argv) > 3 else None
     sym, label, T, KP = KERNELS[kind]
@@ -102,7 +120,7 @@ def main():
     a = next(k for k, l in enumerate(lines) if l.startswith(sym + ":"))
     b = next(k for k in range(a, len(lines)) if "s_endpgm" in lines[k])
     bb = blocks(lines[a:b])
-    parts, wx = loc_parts(bb, T, KP) if kind.startswith("loc") else lds36_parts(bb, T)
+    parts, wx = loc_parts(bb, T, KP, stats) if kind.startswith("loc") else lds36_parts(bb, T)
     valu = collections.Counter()
     lds = collections.Counter()
     for ins, k in parts:
@@ -113,7 +131,7 @@ def main():
                 assert op in LDS_CYC, op
                 lds[op] += k
     d = json.load(open(pmc_path))["counters"]
-    units = B * ITERS
+    units = stats["sum_its"] if stats else B * ITERS  # codeword-iterations of the profiled launch
     total = d["SQ_INSTS_VALU"] / units
     trans = d["SQ_INSTS_VALU_TRANS_F32"] / units
     per = {"packed": valu["packed"], "trans": trans, "plain": total - valu["packed"] - trans}
@@ -123,6 +141,8 @@ def main():
         "kernel": label,
         "kernel_family": label.split("<")[0],
         "git": sha,
+        "codeword_iterations_per_launch": units,
+        "launch_stats": stats,
         "wave_instr_per_codeword_iteration": per,
         "valu_issue_cycles_per_codeword_iteration": sum(per[c] * VALU_CYC[c] for c in VALU_CYC),
         "lds_instr_per_codeword_iteration": dict(lds),
