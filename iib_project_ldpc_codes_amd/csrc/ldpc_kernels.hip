@@ -1617,6 +1617,18 @@ __device__ __forceinline__ bool block_any(int pred, uint32_t *flag, int par) {
     if (threadIdx.x == 0) flag[par ^ 1] = 0u;
     return any;
 }
+// block_any's count form: the number of waves' lanes with pred set (one LDS atomic per wave)
+__device__ __forceinline__ uint32_t block_count(int pred, uint32_t *flag, int par) {
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(pred != 0);
+    if (bal != 0 && (threadIdx.x & (kWave - 1)) == 0) atomicAdd(&flag[par], (uint32_t)__popcll(bal));
+    __syncthreads();
+    const uint32_t c = flag[par];
+    if (threadIdx.x == 0) flag[par ^ 1] = 0u;
+    return c;
+}
+#ifndef LDPC_LOC_EP_W0
+#define LDPC_LOC_EP_W0 48  // early stop with posteriors: slab writes after syndromes with <= this many threads unsatisfied
+#endif
 #ifndef LDPC_LOC_BLOCK_ANY
 #define LDPC_LOC_BLOCK_ANY 1  // bp_loc_kernel early stop: block_any (one barrier) for the stop test
 #endif
@@ -1637,7 +1649,7 @@ template <bool B> using bool_c = std::integral_constant<bool, B>;
 constexpr int loc_waves_per_simd(int T, int KP) { return T == 512 && KP <= 5 ? 4 : 1; }
 
 template <int DLO, int DHI, int DVN0, int DVN1, int KP, int T, int ALGO, bool ABS0, bool ABS1, bool ET = false,
-          bool MC = false>
+          bool MC = false, bool EP = false>
 __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(BpArgs a) {
     static_assert(!ET || ALGO == 0 || DLO == DHI, "min-sum early stop: one check class");
     static_assert(!ET || 2 * 2 * KP <= 64, "early stop keeps the thread's decisions in one 64-bit word");
@@ -1771,7 +1783,13 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     // incoming c->v ratios (min-sum: its posterior sum) of the latest variable phase in the
     // workgroup's slab, a.scratch + blockIdx.x * VP * T float2 (lane-contiguous stores, L2-
     // resident: 40 KB per workgroup); the stopping iteration's posteriors come from there.
-    const bool ep = ET && !MC && a.post != nullptr;
+    // The slab is written only in variable phases that follow a check phase with at most
+    // LDPC_LOC_EP_W0 threads holding an unsatisfied check (frames converge through nearly
+    // satisfied syndromes); a frame that stops without a slab from its last variable phase
+    // is decoded again from its channel LLRs -- the same deterministic trajectory -- with
+    // the slab written in that variable phase (redo_it).
+    static_assert(!EP || (ET && !MC), "EP: early-stop decodes with posteriors");
+    constexpr bool ep = EP;
     float2 *slab = ep ? reinterpret_cast<float2 *>(a.scratch) + (size_t)blockIdx.x * VP * T : nullptr;
     __shared__ int next_b;
     for (int round = 0;; ++round) {
@@ -1780,6 +1798,10 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
         const int b = ep ? __builtin_amdgcn_readfirstlane(next_b) : (int)blockIdx.x + round * (int)gridDim.x;
         if (b >= a.B) break;
         const uint64_t cw = a.first_cw + (uint64_t)b;
+        int redo_it = -1;  // EP: the variable phase whose slab a second pass must write
+    restart:
+        int slab_it = -2;  // EP: the variable phase that last wrote the slab
+        bool slab_now = false;
         if constexpr (ET) {
             if (tid == 0) stop_flag[0] = stop_flag[1] = 0u;  // visible after the staging barrier
         }
@@ -1899,11 +1921,11 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                     at(a1[j - 1]) = R.y;
                     if (j < DV - 1) suf = suf * cv[j - 1];
                 }
-                if (ep) slab[v * T + tid] = loc[v] * suf;  // prod of the incoming c->v ratios
+                if (ep && slab_now) slab[v * T + tid] = loc[v] * suf;  // prod of the incoming c->v ratios
                 loc[v] = sgn(ratio_wire2(DN > 0 ? L[v] * suf : L[v]));
             } else {
                 const float2 s = ms_sum(dn_tag, v, L[v], loc[v], cv);
-                if (ep) slab[v * T + tid] = s;  // the posterior itself
+                if (ep && slab_now) slab[v * T + tid] = s;  // the posterior itself
 #pragma unroll
                 for (int u = 0; u < DN; ++u) {
                     at(a0[u]) = s.x - cv[u].x;
@@ -1970,8 +1992,16 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                 // the syndrome of the previous variable phase's decisions: stop when every
                 // check is satisfied (oracle: after that iteration)
                 if constexpr (SGN_LSB) unsat &= 1;  // the parities are in bit 0 of the OR of the pairs' words
-                const bool more = LDPC_LOC_BLOCK_ANY ? block_any(unsat | (it == 0), stop_flag, it & 1)
-                                                     : __syncthreads_or(unsat | (it == 0));
+                bool more;
+                if constexpr (EP) {
+                    const uint32_t cnt = block_count(unsat | (it == 0), stop_flag, it & 1);
+                    more = cnt != 0u;
+                    slab_now = cnt <= (uint32_t)LDPC_LOC_EP_W0 || it == redo_it;
+                    if (more && slab_now) slab_it = it;
+                } else {
+                    more = LDPC_LOC_BLOCK_ANY ? block_any(unsat | (it == 0), stop_flag, it & 1)
+                                              : __syncthreads_or(unsat | (it == 0));
+                }
                 if (!more) {
                     stopped = true;
                     break;
@@ -2006,6 +2036,11 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             continue;
         }
         if constexpr (ET && !MC) {
+            if (stopped && ep && slab_it != it - 1) {  // no slab from the last variable phase: again
+                redo_it = it - 1;
+                __syncthreads();  // every thread is past its reads of this pass's LDS
+                goto restart;
+            }
             if (stopped && ep) {
                 // posteriors of the stopping iteration from the slab (its last variable phase):
                 // SPA log2 E + log2(prod c->v) -- the oracle's L + sum of the c->v messages -- and
@@ -3598,19 +3633,25 @@ hipError_t launch_generic(const ldpc_graph &g, BpArgs a, hipStream_t s) {
 
 template <int DLO, int DHI, int D0, int D1, bool A0, bool A1, int T, int KP, int ALGO, bool ET, bool MC>
 hipError_t launch_loc_shape(const ldpc_graph &g, BpArgs a, hipStream_t s) {
-    auto k = bp_loc_kernel<DLO, DHI, D0, D1, KP, T, ALGO, A0, A1, ET, MC>;
     const size_t lds = loc_lds_bytes(g, a.max_iters, MC || (ET && ALGO == 1), ET && ALGO == 1);
+    if constexpr (ET && !MC) {
+        if (a.post) {  // early stop with posteriors: persistent grid, slab + counter in scratch
+            auto k = bp_loc_kernel<DLO, DHI, D0, D1, KP, T, ALGO, A0, A1, true, false, true>;
+            hipError_t e = allow_lds(k, lds);
+            if (e != hipSuccess) return e;
+            if (!a.scratch) return hipErrorInvalidValue;
+            const unsigned grid = (unsigned)std::min<int>(a.B, loc_ep_grid());
+            a.work = reinterpret_cast<uint32_t *>(a.scratch + loc_ep_slab_floats(g));
+            e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), s);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, s, a);
+            return hipGetLastError();
+        }
+    }
+    auto k = bp_loc_kernel<DLO, DHI, D0, D1, KP, T, ALGO, A0, A1, ET, MC>;
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
-    unsigned grid = (unsigned)a.B;
-    if (ET && !MC && a.post) {  // early stop with posteriors: persistent grid, slab + counter in scratch
-        if (!a.scratch) return hipErrorInvalidValue;
-        grid = (unsigned)std::min<int>(a.B, loc_ep_grid());
-        a.work = reinterpret_cast<uint32_t *>(a.scratch + loc_ep_slab_floats(g));
-        e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), s);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, s, a);
+    hipLaunchKernelGGL(k, dim3(a.B), dim3(T), lds, s, a);
     return hipGetLastError();
 }
 
