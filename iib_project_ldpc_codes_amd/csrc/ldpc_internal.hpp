@@ -183,7 +183,12 @@ inline int sample_buckets(int E) { return E <= 16384 ? 256 : (E < 65536 ? 512 : 
 #endif
 constexpr int kBigK2Log = LDPC_BIG_K2_LOG, kBigK2 = 1 << kBigK2Log;
 // staging capacity: two u16 arrays beside the [K2][16] counters in 160 KB of LDS
-constexpr int kBigCap = kBigK2Log >= 10 ? 23552 : 31232;
+#ifndef LDPC_BIG_T
+#define LDPC_BIG_T 512  // threads of the two-level sampler (512: two workgroups per CU in 80 KB of LDS)
+#endif
+constexpr int kBigT = LDPC_BIG_T;
+// LDS staging capacity per super-bucket (u16, two arrays); the oracle's BIG_CAP must equal it
+constexpr int kBigCap = kBigT == 1024 ? (kBigK2Log >= 10 ? 23552 : 31232) : 15360;
 inline int big_superbuckets_log2(int E) {
     for (int l = 1; l <= 6; ++l)
         if (((long)E + (1 << l) - 1) / (1 << l) <= kBigCap / 2) return l;

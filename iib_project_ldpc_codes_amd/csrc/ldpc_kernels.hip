@@ -2690,14 +2690,18 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
 // path) rejects the attempt.  oracle_sample_regular / oracle_sample_csr restate
 // it bit for bit.
 template <int LOGK1>
-__global__ __launch_bounds__(1024) void sample_big_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
-                                                         uint64_t first_graph, int32_t *check_lookup,
-                                                         int32_t *variable_lookup, int32_t *attempts,
-                                                         int max_attempts) {
-    constexpr int T = 1024, NW = T / kWave, K2 = kBigK2, LOGK2 = kBigK2Log, K1 = 1 << LOGK1;
+__global__ __launch_bounds__(kBigT) void sample_big_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
+                                                          uint64_t first_graph, int32_t *check_lookup,
+                                                          int32_t *variable_lookup, int32_t *attempts,
+                                                          int max_attempts) {
+    // kBigT threads; level-2 bucket b (of K2) is owned by thread b / BPT (BPT contiguous buckets
+    // per thread, so a scan over threads keeps the bucket-major order) and shuffled with the
+    // Philox stream of its bucket index -- the same permutation for any thread count
+    constexpr int T = kBigT, NW = T / kWave, K2 = kBigK2, LOGK2 = kBigK2Log, K1 = 1 << LOGK1, BPT = K2 / T;
+    static_assert(K2 % T == 0 && K1 <= T, "bucket ownership");
     extern __shared__ __align__(16) unsigned char smem[];
-    int *cnt2 = reinterpret_cast<int *>(smem);  // [K2][NW]
-    int *cnt1 = cnt2 + K2 * NW;                  // [K1][NW]
+    uint16_t *cnt2 = reinterpret_cast<uint16_t *>(smem);  // [K2][NW] (counts and offsets < kBigCap)
+    int *cnt1 = reinterpret_cast<int *>(smem + (size_t)K2 * NW * 2);  // [K1][NW]
     int *wsum = cnt1 + K1 * NW;                  // [16]
     int *sst = wsum + 16;                        // [K1 + 1] super-bucket starts
     uint16_t *A = reinterpret_cast<uint16_t *>(sst + 68);
@@ -2733,18 +2737,71 @@ __global__ __launch_bounds__(1024) void sample_big_kernel(SampleShape sh, uint32
             }
         }
     };
-    // counts -> offsets, bucket-major / wave-minor; returns this thread's bucket start/size
-    auto offsets = [&](int *cnt, int K, int &start, int &size) {
+    // level-1 pass without LDS traffic: lane b (< K1) of each wave keeps the running count
+    // (count pass) or next offset (scatter pass) of bucket b for its wave in a VGPR.  From the
+    // group's LOGK1 uniform bit ballots every lane forms both its own peers mask (its rank)
+    // and the mask of bucket `lane` (that bucket's count in the group); a socket's slot is
+    // lane bk's offset (ds_bpermute) + its rank.  Same stable order as pass() + LDS counters.
+    auto pass1 = [&](uint32_t c1, bool scatter, int &reg) {
+        const int S = E;
+        const int chunk = ((S + NW - 1) / NW + 255) / 256 * 256;
+        const int lo = min(S, wave * chunk), hi = min(S, lo + chunk);
+        for (int b256 = lo; b256 < hi; b256 += 256) {
+            const uint4 r = philox_block((uint32_t)(((b256 >> 8) << 6) | lane), c1, g0, g1, k0, k1);
+            for (int base = b256; base < min(hi, b256 + 256); base += 64) {
+                const int s = base + lane;
+                const bool valid = s < hi;
+                const uint32_t bk = valid ? pick4(r, (base >> 6) & 3) >> (32 - LOGK1) : 0u;
+                const uint64_t vmask = __ballot(valid);
+                uint64_t peers = vmask, mine = vmask;
+#pragma unroll
+                for (int bit = 0; bit < LOGK1; ++bit) {
+                    const uint64_t bal = __ballot(valid && ((bk >> bit) & 1u));
+                    peers &= ((bk >> bit) & 1u) ? bal : ~bal;
+                    mine &= ((lane >> bit) & 1) ? bal : ~bal;
+                }
+                if (scatter) {
+                    const int off = __shfl(reg, (int)bk, kWave);
+                    if (valid) L1[off + __popcll(peers & lt_mask)] = (uint16_t)(csr ? sh.vsock[s] : s / dv);
+                }
+                reg += __popcll(mine);
+            }
+        }
+    };
+    // level 1: counts -> offsets, bucket-major / wave-minor (thread b < K1 owns bucket b)
+    auto offsets1 = [&](int &start, int &size) {
         size = 0;
-        if (tid < K)
-            for (int w = 0; w < NW; ++w) size += cnt[tid * NW + w];
+        if (tid < K1)
+            for (int w = 0; w < NW; ++w) size += cnt1[tid * NW + w];
         int total = 0;
         start = block_excl_scan(size, wsum, total);
-        if (tid < K) {
+        if (tid < K1) {
             int run = start;
             for (int w = 0; w < NW; ++w) {
-                const int c = cnt[tid * NW + w];
-                cnt[tid * NW + w] = run;
+                const int c = cnt1[tid * NW + w];
+                cnt1[tid * NW + w] = run;
+                run += c;
+            }
+        }
+        __syncthreads();
+    };
+    // level 2: thread tid owns buckets tid*BPT .. +BPT; their starts / sizes
+    auto offsets2 = [&](int (&st)[BPT], int (&sz)[BPT]) {
+        int size = 0;
+#pragma unroll
+        for (int j = 0; j < BPT; ++j) {
+            sz[j] = 0;
+            for (int w = 0; w < NW; ++w) sz[j] += cnt2[(tid * BPT + j) * NW + w];
+            size += sz[j];
+        }
+        int total = 0;
+        int run = block_excl_scan(size, wsum, total);
+#pragma unroll
+        for (int j = 0; j < BPT; ++j) {
+            st[j] = run;
+            for (int w = 0; w < NW; ++w) {
+                const int c = cnt2[(tid * BPT + j) * NW + w];
+                cnt2[(tid * BPT + j) * NW + w] = (uint16_t)run;
                 run += c;
             }
         }
@@ -2756,20 +2813,16 @@ __global__ __launch_bounds__(1024) void sample_big_kernel(SampleShape sh, uint32
     while (!ok && att < max_attempts) {
         const uint32_t ca = kSampleTag | ((uint32_t)att << 2);
         // ---- level 1
-        for (int i = tid; i < K1 * NW; i += T) cnt1[i] = 0;
-        __syncthreads();
-        pass(E, ca | 2u, LOGK1, [&](int, int bk, int rank, uint64_t peers) {
-            if (rank == 0) cnt1[bk * NW + wave] += __popcll(peers);
-        });
+        int reg = 0;
+        pass1(ca | 2u, false, reg);
+        if (lane < K1) cnt1[lane * NW + wave] = reg;
         __syncthreads();
         int st1, sz1;
-        offsets(cnt1, K1, st1, sz1);
+        offsets1(st1, sz1);
         if (tid < K1) sst[tid] = st1;
         if (tid == 0) sst[K1] = E;
-        pass(E, ca | 2u, LOGK1, [&](int s, int bk, int rank, uint64_t peers) {
-            L1[cnt1[bk * NW + wave] + rank] = (uint16_t)(csr ? sh.vsock[s] : s / dv);
-            if (rank == 0) cnt1[bk * NW + wave] += __popcll(peers);
-        });
+        reg = lane < K1 ? cnt1[lane * NW + wave] : 0;
+        pass1(ca | 2u, true, reg);
         __threadfence_block();
         __syncthreads();
         // ---- level 2, super-bucket by super-bucket, validating finished checks
@@ -2786,24 +2839,27 @@ __global__ __launch_bounds__(1024) void sample_big_kernel(SampleShape sh, uint32
             for (int x = tid; x < K2 * NW; x += T) cnt2[x] = 0;
             __syncthreads();
             pass(S, ci, LOGK2, [&](int, int bk, int rank, uint64_t peers) {
-                if (rank == 0) cnt2[bk * NW + wave] += __popcll(peers);
+                if (rank == 0) cnt2[bk * NW + wave] += (uint16_t)__popcll(peers);
             });
             __syncthreads();
-            int st2, sz2;
-            offsets(cnt2, K2, st2, sz2);
+            int st2[BPT], sz2[BPT];
+            offsets2(st2, sz2);
             pass(S, ci, LOGK2, [&](int s, int bk, int rank, uint64_t peers) {
                 Bf[cnt2[bk * NW + wave] + rank] = A[s];
-                if (rank == 0) cnt2[bk * NW + wave] += __popcll(peers);
+                if (rank == 0) cnt2[bk * NW + wave] += (uint16_t)__popcll(peers);
             });
             __syncthreads();
-            if (tid < K2 && !(LDPC_SAMPLER_SKIP & 2)) {
-                BucketRng rng{k0, k1, (uint32_t)tid << 20, ci | 1u, g0, g1};
-                uint16_t *bb = Bf + st2;
-                for (int x = sz2 - 1; x >= 1; --x) {
-                    const int j = (int)rng.below((uint32_t)x + 1u);
-                    const uint16_t t = bb[x];
-                    bb[x] = bb[j];
-                    bb[j] = t;
+            if (!(LDPC_SAMPLER_SKIP & 2)) {
+#pragma unroll
+                for (int j = 0; j < BPT; ++j) {
+                    BucketRng rng{k0, k1, (uint32_t)(tid * BPT + j) << 20, ci | 1u, g0, g1};
+                    uint16_t *bb = Bf + st2[j];
+                    for (int x = sz2[j] - 1; x >= 1; --x) {
+                        const int jj = (int)rng.below((uint32_t)x + 1u);
+                        const uint16_t t = bb[x];
+                        bb[x] = bb[jj];
+                        bb[jj] = t;
+                    }
                 }
             }
             __syncthreads();
@@ -3889,12 +3945,13 @@ static hipError_t launch_sample(const SampleShape &sh, uint64_t seed, uint64_t f
     if (K == 512 && u16) LDPC_SAMPLE(512, uint16_t, true);
     const int logk1 = big_superbuckets_log2(E);
     if (u16 && logk1 > 0) {
-        const size_t lds = (size_t)4 * (kBigK2 * 16 + (1 << logk1) * 16 + 16 + 68) + (size_t)4 * kBigCap;
+        const size_t lds = (size_t)2 * kBigK2 * (kBigT / kWave) + (size_t)4 * ((1 << logk1) * (kBigT / kWave) + 16 + 68) +
+                           (size_t)4 * kBigCap;
 #define LDPC_BIG(L)                                                                                            \
     case L: {                                                                                                  \
         hipError_t e = allow_lds(sample_big_kernel<L>, lds);                                                   \
         if (e != hipSuccess) return e;                                                                         \
-        hipLaunchKernelGGL(sample_big_kernel<L>, dim3(G), dim3(1024), lds, stream, sh, k0, k1, first_graph,    \
+        hipLaunchKernelGGL(sample_big_kernel<L>, dim3(G), dim3(kBigT), lds, stream, sh, k0, k1, first_graph,   \
                            check_lookup, variable_lookup, attempts, max_attempts);                             \
         return hipGetLastError();                                                                              \
     }
