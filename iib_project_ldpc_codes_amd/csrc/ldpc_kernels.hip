@@ -74,7 +74,8 @@ constexpr int kWave = 64;
 #define LDPC_SAMPLER_FIXED_ATT 0  // timing ablation only: exactly this many permutations per graph
 #endif
 #ifndef LDPC_SAMPLER_SKIP
-#define LDPC_SAMPLER_SKIP 0       // timing ablation only: 2 = no Fisher-Yates, 8 = no variable_lookup
+#define LDPC_SAMPLER_SKIP 0       // timing ablation only: 2 = no Fisher-Yates, 8 = no variable_lookup,
+                                  // 16 = no level 2 (big), 32 = no level-1 scatter (big), 64 = one super-bucket
 #endif
 
 // ---------------------------------------------------------------------------
@@ -2822,13 +2823,13 @@ __global__ __launch_bounds__(kBigT) void sample_big_kernel(SampleShape sh, uint3
         if (tid < K1) sst[tid] = st1;
         if (tid == 0) sst[K1] = E;
         reg = lane < K1 ? cnt1[lane * NW + wave] : 0;
-        pass1(ca | 2u, true, reg);
+        if (!(LDPC_SAMPLER_SKIP & 32)) pass1(ca | 2u, true, reg);
         __threadfence_block();
         __syncthreads();
         // ---- level 2, super-bucket by super-bucket, validating finished checks
         bool bad = false;
         int done = 0;  // checks validated so far
-        for (int i = 0; i < K1 && !bad; ++i) {
+        for (int i = 0; i < ((LDPC_SAMPLER_SKIP & 16) ? 0 : (LDPC_SAMPLER_SKIP & 64) ? 1 : K1) && !bad; ++i) {
             const int st = sst[i], S = sst[i + 1] - st;
             if (S > kBigCap) {
                 bad = true;

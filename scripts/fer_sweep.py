@@ -3,6 +3,8 @@
   cfg3: (3,6) n=10000, BSC, normalized min-sum, crossover sweep, ~1M trials per point
   cfg4: RSU rate-1/2 irregular (ring degree-2 placement, ensembles.py deg2="path"), n=20000,
         BI-AWGN, SPA, 100 it
+  ens:  BASELINE configs[4] -- expurgated (3,6) ensemble (a fresh device-sampled graph per
+        trial, parallel_simulator_expurgated.py), n=64800, BEC, 200 it, expurgation X=3
 One process per GPU (torchrun); trials shard by index, counters all-reduced per round.
 Each point stops at --stop-errors frame errors (200, parallel_simulator.py:198), --trials,
 or --seconds.
@@ -28,7 +30,7 @@ from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("config", choices=["cfg3", "cfg4"])
+    ap.add_argument("config", choices=["cfg3", "cfg4", "ens"])
     ap.add_argument("--trials", type=int, default=1_000_000)
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--batch", type=int, default=None)
@@ -38,6 +40,7 @@ def main():
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--stop-errors", type=int, default=200)
     ap.add_argument("--deg2", default="path", help="cfg4 degree-2 placement (ensembles.sample_irregular)")
+    ap.add_argument("--expurgation", type=int, default=3, help="ens: X (parallel_simulator_expurgated.py argv[9])")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -50,14 +53,24 @@ def main():
         channel, algo, alpha, iters = "bsc", "minsum", 0.75, 50
         points = [float(p) for p in (args.points or "0.07,0.065,0.06,0.055,0.05").split(",")]
         batch = args.batch or 65536
+    elif args.config == "ens":
+        g = None
+        channel, algo, alpha, iters = "bec", "spa", 1.0, 200
+        points = [float(p) for p in (args.points or "0.425,0.42").split(",")]
+        batch = args.batch or 16384
     else:
         g = ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1, deg2=args.deg2)
         channel, algo, alpha, iters = "awgn", "spa", 1.0, 100
         points = [float(p) for p in (args.points or "0.86,0.84,0.82,0.80,0.78").split(",")]
         batch = args.batch or 16384
-    rate = 1.0 - g.m / g.n
+    n, rate = (64800, 0.5) if g is None else (g.n, 1.0 - g.m / g.n)
     for p in points:
-        mc = MonteCarlo(g, channel, p, iters, algo=algo, alpha=alpha, early_stop=True, seed=args.seed, batch=batch)
+        if g is None:
+            mc = MonteCarlo.ensemble(n, 3, 6, channel, p, iters, expurgation=args.expurgation, seed=args.seed,
+                                     batch=batch)
+        else:
+            mc = MonteCarlo(g, channel, p, iters, algo=algo, alpha=alpha, early_stop=True, seed=args.seed,
+                            batch=batch)
         ck = None
         if args.checkpoint_dir:
             os.makedirs(args.checkpoint_dir, exist_ok=True)
@@ -71,8 +84,8 @@ def main():
         torch.cuda.synchronize()
         el = time.time() - t0
         if rank == 0:
-            out = {"config": args.config, "deg2": args.deg2 if args.config == "cfg4" else None, "channel": channel, "param": p, "algo": algo, "iterations": iters,
-                   "n": g.n, "rate": rate, "gpus": world, "trials": res["num_tests"],
+            out = {"config": args.config, "expurgation": mc.expurgation, "deg2": args.deg2 if args.config == "cfg4" else None, "channel": channel, "param": p, "algo": algo, "iterations": iters,
+                   "n": n, "rate": rate, "gpus": world, "trials": res["num_tests"],
                    "frame_errors": res["frame_errors"], "fer": res["fer"], "ber": res["ber"],
                    "mean_iterations": res["iterations"] / max(res["num_tests"], 1),
                    "seconds": el, "codewords_per_s": (res["num_tests"] - trials0) / el}

@@ -44,16 +44,20 @@ from valu_mix import blocks, mix  # noqa: E402
 N, DV, DC, B, ITERS = 10000, 3, 6, 65536, 50
 LDS_CYC = {"ds_read_b128": 4, "ds_write_b128": 13, "ds_read_b32": 2, "ds_write_b32": 4,
            "ds_read_b64": 2, "ds_write_b64": 6, "ds_write2st64_b32": 8, "ds_write2_b32": 8,
-           "ds_read2_b32": 4, "ds_read2st64_b32": 4}
+           "ds_read2_b32": 4, "ds_read2st64_b32": 4, "ds_read2_b64": 4, "ds_write2_b64": 13,
+           "ds_read_u8": 2, "ds_write_b8": 4, "ds_read_u16": 2, "ds_write_b16": 4, "ds_bpermute_b32": 2,
+           "ds_swizzle_b32": 2, "ds_add_u32": 4, "ds_or_b32": 4, "ds_read_b96": 4, "ds_write_b96": 13}
 VALU_CYC = {"packed": 4.0, "plain": 2.0, "trans": 8.0}
 KERNELS = {
-    "loc": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi5ELi512ELi0ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
+    "loc": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi5ELi512ELi0ELb0ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
             "bp_loc_kernel<6,6,2,2,KP=5,T=512,SPA,fixed-count>", 512, 5),
-    "loc1024": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi3ELi1024ELi0ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
+    "loc1024": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi3ELi1024ELi0ELb0ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
                 "bp_loc_kernel<6,6,2,2,KP=3,T=1024,SPA,fixed-count>", 1024, 3),
-    "loc_et": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi5ELi512ELi0ELb0ELb0ELb1ELb0EEEvNS0_6BpArgsE",
+    "loc_et": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi5ELi512ELi0ELb0ELb0ELb1ELb0ELb0EEEvNS0_6BpArgsE",
                "bp_loc_kernel<6,6,2,2,KP=5,T=512,SPA,early-stop>", 512, 5),
-    "loc_ms": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi5ELi512ELi1ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
+    "loc_ep": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi5ELi512ELi0ELb0ELb0ELb1ELb0ELb1EEEvNS0_6BpArgsE",
+               "bp_loc_kernel<6,6,2,2,KP=5,T=512,SPA,early-stop+posteriors>", 512, 5),
+    "loc_ms": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi5ELi512ELi1ELb0ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
                "bp_loc_kernel<6,6,2,2,KP=5,T=512,min-sum,fixed-count>", 512, 5),
     "lds36": ("_ZN4ldpc12_GLOBAL__N_113bp_lds_kernelILi3ELi6ELi1024ELi10ELi0ELb0ELb0EEEvNS0_6BpArgsE",
               "bp_lds_kernel<3,6,1024,10,SPA,fixed-count>", 1024, None),
@@ -72,19 +76,31 @@ def loc_parts(bb, T, KP, stats=None):
         r_cw = stats["batch"] / stats["sum_its"]
     else:
         r_chk, r_var, r_cw = 1.0, (ITERS - 1) / ITERS, 1.0 / ITERS
-    chk = [i for i, (_, ins) in enumerate(bb) if ins.count("ds_read_b128") == 2 and ins.count("ds_write_b128") == 2]
+    # check slot k: the block storing the pair's two ds_write_b128 (the early-stop builds load
+    # one of the two b128 inputs as a b128 and the other through two narrower reads)
+    chk = [i for i, (_, ins) in enumerate(bb) if ins.count("ds_write_b128") == 2]
     assert len(chk) == KP, len(chk)
-    var = max(range(len(bb)), key=lambda i: bb[i][1].count("ds_read_b32"))
-    assert bb[var][1].count("ds_read_b32") == 8 * KP and bb[var][1].count("ds_write_b32") == 8 * KP
+    # variable phase: the blocks after the check slots holding its 8*KP ds_read_b32 / ds_write_b32
+    # (one block; split in ten by the slab-store branches in the early-stop-with-posteriors build)
+    var, nr = [], 0
+    for i in range(chk[-1] + 1, len(bb)):
+        ins = bb[i][1]
+        if ins.count("ds_read_b32") >= 4 and ins.count("ds_write_b32") >= 4:
+            var.append(i)
+            nr += ins.count("ds_read_b32")
+            if nr >= 8 * KP:
+                break
+    assert nr == 8 * KP and sum(bb[i][1].count("ds_write_b32") for i in var) == 8 * KP, (var, nr)
     execs = {}
     for k, i in enumerate(chk):
         lanes = min(max(P - k * T, 0), T)
         execs[i] = (lanes + 63) // 64 * r_chk
-    execs[var] = waves * r_var
+    for i in var:
+        execs[i] = waves * r_var
     parts = []
     for i, (_, ins) in enumerate(bb):
         parts.append((ins, execs.get(i, waves * r_cw)))
-    return parts, {"check_slot_waves": [execs[i] for i in chk], "variable": execs[var],
+    return parts, {"check_slot_waves": [execs[i] for i in chk], "variable": execs[var[0]], "variable_blocks": len(var),
                    "other_blocks": waves * r_cw}
 
 
