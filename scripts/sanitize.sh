@@ -17,4 +17,5 @@ export ASAN_OPTIONS=detect_leaks=0:abort_on_error=1:halt_on_error=1:detect_odr_v
 export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1
 cd "$ROOT"
 LD_PRELOAD="$ASAN_RT $UBSAN_RT" python -m pytest -q -p no:cacheprovider -m "not gpu" \
-  tests/test_host.py tests/test_oracle_golden.py tests/test_ml_oracle.py tests/test_ensembles.py "$@"
+  tests/test_host.py tests/test_oracle_golden.py tests/test_ml_oracle.py tests/test_ensembles.py \
+  tests/test_mc_plan.py tests/test_loc_layout.py "$@"
