@@ -916,11 +916,18 @@ int ldpc_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_gra
 // [vsock E | cptr m+1 | vptr n+1] on the workspace of `stream` (caller holds g_mu).
 static int csr_shape_upload(int n, int m, const int32_t *var_ptr, const int32_t *check_ptr, Workspace &ws,
                             void *stream, int *E_out, const int32_t **vsock, const int32_t **cptr,
-                            const int32_t **vptr) {
+                            const int32_t **vptr, int *max_cdeg, int *max_vdeg) {
     LDPC_REQUIRE(n > 0 && m > 0 && var_ptr && check_ptr, "bad degree structure");
     LDPC_REQUIRE(var_ptr[0] == 0 && check_ptr[0] == 0, "var_ptr / check_ptr must start at 0");
-    for (int v = 0; v < n; ++v) LDPC_REQUIRE(var_ptr[v + 1] >= var_ptr[v], "var_ptr must be non-decreasing");
-    for (int c = 0; c < m; ++c) LDPC_REQUIRE(check_ptr[c + 1] >= check_ptr[c], "check_ptr must be non-decreasing");
+    *max_cdeg = *max_vdeg = 0;
+    for (int v = 0; v < n; ++v) {
+        LDPC_REQUIRE(var_ptr[v + 1] >= var_ptr[v], "var_ptr must be non-decreasing");
+        *max_vdeg = std::max(*max_vdeg, var_ptr[v + 1] - var_ptr[v]);
+    }
+    for (int c = 0; c < m; ++c) {
+        LDPC_REQUIRE(check_ptr[c + 1] >= check_ptr[c], "check_ptr must be non-decreasing");
+        *max_cdeg = std::max(*max_cdeg, check_ptr[c + 1] - check_ptr[c]);
+    }
     const int E = var_ptr[n];
     LDPC_REQUIRE(E > 0 && E == check_ptr[m], "socket counts differ: var_ptr[n] != check_ptr[m]");
     std::vector<int32_t> h((size_t)E + m + 1 + n + 1);
@@ -949,11 +956,11 @@ int ldpc_sample_csr_dev(int n, int m, const int32_t *var_ptr, const int32_t *che
     std::lock_guard<std::mutex> lk(g_mu);
     Workspace &ws = workspace(stream);
     std::lock_guard<std::mutex> wl(ws.mu);
-    int E = 0;
+    int E = 0, mxc = 0, mxv = 0;
     const int32_t *vs, *cp, *vp;
-    rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, stream, &E, &vs, &cp, &vp);
+    rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, stream, &E, &vs, &cp, &vp, &mxc, &mxv);
     if (rc) return rc;
-    LDPC_HIP(launch_sample_csr(n, m, E, vs, cp, vp, seed, first_graph, G, d_check_var, d_var_slot, d_attempts,
+    LDPC_HIP(launch_sample_csr(n, m, E, vs, cp, vp, mxc, mxv, seed, first_graph, G, d_check_var, d_var_slot, d_attempts,
                                1 << 20, static_cast<hipStream_t>(stream)));
     return LDPC_OK;
 }
@@ -966,14 +973,14 @@ int ldpc_sample_csr(int n, int m, const int32_t *var_ptr, const int32_t *check_p
     std::lock_guard<std::mutex> lk(g_mu);
     Workspace &ws = workspace(nullptr);
     std::lock_guard<std::mutex> wl(ws.mu);
-    int E = 0;
+    int E = 0, mxc = 0, mxv = 0;
     const int32_t *vs, *cp, *vp;
-    rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, nullptr, &E, &vs, &cp, &vp);
+    rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, nullptr, &E, &vs, &cp, &vp, &mxc, &mxv);
     if (rc) return rc;
     LDPC_HIP(ws.gchk.ensure((size_t)E * G * 4));
     LDPC_HIP(ws.gvar.ensure((size_t)E * G * 4));
     LDPC_HIP(ws.gatt.ensure((size_t)G * 4 + 4));
-    LDPC_HIP(launch_sample_csr(n, m, E, vs, cp, vp, seed, first_graph, G, static_cast<int32_t *>(ws.gchk.p),
+    LDPC_HIP(launch_sample_csr(n, m, E, vs, cp, vp, mxc, mxv, seed, first_graph, G, static_cast<int32_t *>(ws.gchk.p),
                                static_cast<int32_t *>(ws.gvar.p), static_cast<int32_t *>(ws.gatt.p), 1 << 20,
                                nullptr));
     LDPC_HIP(hipDeviceSynchronize());

@@ -175,25 +175,10 @@ hipError_t launch_mc_reduce(const int32_t *trial, const int32_t *trial_its, int 
 // sockets; the permutation is in LDS (u16) when n*dv < 65536.  Must match
 // oracle_sample_regular.
 inline int sample_buckets(int E) { return E <= 16384 ? 256 : (E < 65536 ? 512 : 1024); }
-// Two-level sampler for n*dv >= 65536 (and n <= 65536): 1024 level-2 buckets,
-// LDS staging capacity per super-bucket, and log2 of the super-bucket count
-// (smallest K1 = 2..64 with mean super-bucket <= capacity / 2; 0 = not usable).
-#ifndef LDPC_BIG_K2_LOG
-#define LDPC_BIG_K2_LOG 10  // level-2 buckets of the two-level sampler (10: all 1024 threads shuffle, 14 % faster than 9)
-#endif
-constexpr int kBigK2Log = LDPC_BIG_K2_LOG, kBigK2 = 1 << kBigK2Log;
-// staging capacity: two u16 arrays beside the [K2][16] counters in 160 KB of LDS
-#ifndef LDPC_BIG_T
-#define LDPC_BIG_T 512  // threads of the two-level sampler (512: two workgroups per CU in 80 KB of LDS)
-#endif
-constexpr int kBigT = LDPC_BIG_T;
-// LDS staging capacity per super-bucket (u16, two arrays); the oracle's BIG_CAP must equal it
-constexpr int kBigCap = kBigT == 1024 ? (kBigK2Log >= 10 ? 23552 : 31232) : 15360;
-inline int big_superbuckets_log2(int E) {
-    for (int l = 1; l <= 6; ++l)
-        if (((long)E + (1 << l) - 1) / (1 << l) <= kBigCap / 2) return l;
-    return 0;
-}
+// Sequential-draw sampler (sample_seq_kernel, one wave per graph) for
+// kSeqMinE <= n*dv <= kSeqMaxE with check degrees <= kSeqMaxCdeg; the oracle's
+// SEQ_* constants must equal these.  Larger graphs: one level, K = 1024.
+constexpr int kSeqMinE = 65536, kSeqMaxE = 393216, kSeqMaxCdeg = 192;
 
 // Random regular graphs on the device (law of random_code_generator.c), one
 // workgroup per graph; attempts[g] = number of permutations drawn (negative if
@@ -204,8 +189,9 @@ hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t 
 // Irregular form: socket s of variable d_vsock[s]; check c owns slots [cptr[c], cptr[c+1]);
 // outputs check_var[g][E] and var_slot[g][E] (CSR, each variable's slots ascending).
 hipError_t launch_sample_csr(int n, int m, int E, const int32_t *d_vsock, const int32_t *d_cptr,
-                             const int32_t *d_vptr, uint64_t seed, uint64_t first_graph, int G, int32_t *check_var,
-                             int32_t *var_slot, int32_t *attempts, int max_attempts, hipStream_t stream);
+                             const int32_t *d_vptr, int max_cdeg, int max_vdeg, uint64_t seed, uint64_t first_graph,
+                             int G, int32_t *check_var, int32_t *var_slot, int32_t *attempts, int max_attempts,
+                             hipStream_t stream);
 // BEC Monte-Carlo where trial b decodes on graph b of (check_lookup, variable_lookup).
 hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,
                                   float p, uint64_t seed, uint64_t first_cw, int B, int max_iters, int32_t *trial,

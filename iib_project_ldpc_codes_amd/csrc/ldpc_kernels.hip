@@ -70,14 +70,6 @@ constexpr int kWave = 64;
 #ifndef LDPC_ABLATE_PHASE
 #define LDPC_ABLATE_PHASE 0    // timing ablation only: 1 = skip the check phase, 2 = skip the variable phase
 #endif
-#ifndef LDPC_SAMPLER_FIXED_ATT
-#define LDPC_SAMPLER_FIXED_ATT 0  // timing ablation only: exactly this many permutations per graph
-#endif
-#ifndef LDPC_SAMPLER_SKIP
-#define LDPC_SAMPLER_SKIP 0       // timing ablation only: 2 = no Fisher-Yates, 8 = no variable_lookup,
-                                  // 16 = no level 2 (big), 32 = no level-1 scatter (big), 64 = one super-bucket
-#endif
-
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (the rocRAND philox4x32_10 stream: rocrand_init(seed,
 // subsequence = codeword, offset = 4*g) -> rocrand4 == philox_block(g, 0,
@@ -2678,225 +2670,273 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
     }
 }
 
-// Large graphs (n*dv >= 65536, n <= 65536): two-level Rao-Sandelius, still
-// exactly uniform.  Level 1 splits all sockets into K1 super-buckets (draws
-// ctr {(s>>8)<<6 | s&63, tag|att<<2|2, g}; stable scatter of variable ids as
-// u16 into the variable_lookup row, used as scratch); super-bucket i is then
-// staged into LDS and permuted by the one-level scheme with 1024 buckets (draws
-// ctr {.., tag|i<<22|att<<2|0, g}, Fisher-Yates streams {t<<20|blk,
-// tag|i<<22|att<<2|1, g}) and written to its slot range.  Checks are validated
-// as soon as all their slots are final, so a bad attempt usually stops after a
-// few super-buckets.  A super-bucket larger than the LDS staging capacity
-// (kBigCap, > 2x the mean -- probability < e^-4000 at the sizes that use this
-// path) rejects the attempt.  oracle_sample_regular / oracle_sample_csr restate
-// it bit for bit.
-template <int LOGK1>
-__global__ __launch_bounds__(kBigT) void sample_big_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
-                                                          uint64_t first_graph, int32_t *check_lookup,
-                                                          int32_t *variable_lookup, int32_t *attempts,
-                                                          int max_attempts) {
-    // kBigT threads; level-2 bucket b (of K2) is owned by thread b / BPT (BPT contiguous buckets
-    // per thread, so a scan over threads keeps the bucket-major order) and shuffled with the
-    // Philox stream of its bucket index -- the same permutation for any thread count
-    constexpr int T = kBigT, NW = T / kWave, K2 = kBigK2, LOGK2 = kBigK2Log, K1 = 1 << LOGK1, BPT = K2 / T;
-    static_assert(K2 % T == 0 && K1 <= T, "bucket ownership");
+// Large graphs (65536 <= n*dv <= kSeqMaxE): sequential-draw sampler, one wave per
+// graph.  The same law -- a uniform socket permutation conditioned on every check
+// being simple -- drawn slot by slot, so a bad check is seen as soon as its last
+// slot is drawn and the attempt stops there (a failing (3,6) attempt at n = 64,800
+// stops after ~1/5 of the graph instead of paying a whole permutation):
+//   * slot x (in order) takes a uniform unused entry of the pool: words of the
+//     Philox stream ctr {x | blk<<24, tag|att<<2|3, g_lo, g_hi} give Lemire draws
+//     on [0, R) until one lands on an unused pool index (a bitmap in LDS);
+//     1024 words without one reject the attempt (probability < (3/4)^1000);
+//   * the pool starts as all R = E sockets; when R' = ceil(R/4) entries are left
+//     the unused ones are compacted in order into a new pool (global scratch,
+//     the variable_lookup row) with a fresh bitmap, so no draw ever sees more
+//     than 3/4 of its pool used; the last <= kSeqFinal entries are
+//     Fisher-Yates-shuffled by one lane (stream {blk, tag|1<<30|att<<2|3, g});
+//   * 64 consecutive slots are drawn per round, one per lane, against the bitmap
+//     of the slots before the round; an LDS atomic OR marks the picks, and when
+//     two lanes picked the same entry the round keeps only the lanes below the
+//     second-lowest lane of every such group (the later lanes redraw next round
+//     from the updated bitmap -- a slot's result is its first draw not used by an
+//     earlier slot, exactly the sequential process);
+//   * every check whose slots are all drawn is tested (variable ids kept in an
+//     LDS ring of the last kSeqRing slots); a repeat redraws from slot 0 (att+1).
+// ~25.6 KB of LDS per wave at n = 64,800 (the bitmap), so six graphs per CU.
+// The variable side is built with per-variable occurrence counters packed fb bits
+// per variable into the bitmap's LDS (fb = 0: global CAS, sample_emit_var_side).
+// oracle_sample_regular / oracle_sample_csr restate it bit for bit.
+constexpr int kSeqFinal = 64, kSeqRing = 256;
+
+__device__ __forceinline__ int wave_excl_scan(int v, int &total) {
+    const int lane = threadIdx.x & 63;
+    int incl = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const int y = __shfl_up(incl, d, kWave);
+        if (lane >= d) incl += y;
+    }
+    total = __shfl(incl, kWave - 1, kWave);
+    return incl - v;
+}
+
+__global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
+                                                           uint64_t first_graph, int32_t *check_lookup,
+                                                           int32_t *variable_lookup, int32_t *attempts,
+                                                           int max_attempts, int bw, int fb) {
     extern __shared__ __align__(16) unsigned char smem[];
-    uint16_t *cnt2 = reinterpret_cast<uint16_t *>(smem);  // [K2][NW] (counts and offsets < kBigCap)
-    int *cnt1 = reinterpret_cast<int *>(smem + (size_t)K2 * NW * 2);  // [K1][NW]
-    int *wsum = cnt1 + K1 * NW;                  // [16]
-    int *sst = wsum + 16;                        // [K1 + 1] super-bucket starts
-    uint16_t *A = reinterpret_cast<uint16_t *>(sst + 68);
-    uint16_t *Bf = A + kBigCap;
+    uint32_t *bm = reinterpret_cast<uint32_t *>(smem);  // [bw] pool bitmap, later rank counters
+    int *ring = reinterpret_cast<int *>(bm + bw);       // [kSeqRing] variable of slot x at x % kSeqRing
+    int *fin = ring + kSeqRing;                         // [kSeqFinal] last pool entries
     const int n = sh.n, E = sh.E, m = sh.m, dv = sh.dv, dc = sh.dc;
     const bool csr = sh.vsock != nullptr;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lane = threadIdx.x;
     const uint64_t gid = first_graph + blockIdx.x;
     const uint32_t g0 = (uint32_t)gid, g1 = (uint32_t)(gid >> 32);
     int32_t *out = check_lookup + (size_t)blockIdx.x * E;
-    uint16_t *L1 = reinterpret_cast<uint16_t *>(variable_lookup + (size_t)blockIdx.x * E);
-    const uint64_t lt_mask = (1ull << lane) - 1;
-    (void)n;
-
-    // one-level pass over [0, S) split into per-wave chunks: bucket of element s from
-    // word (s>>6)&3 of Philox {(s>>8)<<6 | lane, c1, g}, top LOGK bits; f(s, bk, rank, peers)
-    auto pass = [&](int S, uint32_t c1, int logk, auto &&f) {
-        const int chunk = ((S + NW - 1) / NW + 255) / 256 * 256;
-        const int lo = min(S, wave * chunk), hi = min(S, lo + chunk);
-        for (int b256 = lo; b256 < hi; b256 += 256) {
-            const uint4 r = philox_block((uint32_t)(((b256 >> 8) << 6) | lane), c1, g0, g1, k0, k1);
-            for (int base = b256; base < min(hi, b256 + 256); base += 64) {
-                const int s = base + lane;
-                const bool valid = s < hi;
-                const uint32_t bk = valid ? pick4(r, (base >> 6) & 3) >> (32 - logk) : 0u;
-                uint64_t peers = __ballot(valid);
-                for (int bit = 0; bit < logk; ++bit) {
-                    const bool on = (bk >> bit) & 1u;
-                    const uint64_t bal = __ballot(valid && on);
-                    peers &= on ? bal : ~bal;
-                }
-                if (valid) f(s, (int)bk, __popcll(peers & lt_mask), peers);
-            }
-        }
-    };
-    // level-1 pass without LDS traffic: lane b (< K1) of each wave keeps the running count
-    // (count pass) or next offset (scatter pass) of bucket b for its wave in a VGPR.  From the
-    // group's LOGK1 uniform bit ballots every lane forms both its own peers mask (its rank)
-    // and the mask of bucket `lane` (that bucket's count in the group); a socket's slot is
-    // lane bk's offset (ds_bpermute) + its rank.  Same stable order as pass() + LDS counters.
-    auto pass1 = [&](uint32_t c1, bool scatter, int &reg) {
-        const int S = E;
-        const int chunk = ((S + NW - 1) / NW + 255) / 256 * 256;
-        const int lo = min(S, wave * chunk), hi = min(S, lo + chunk);
-        for (int b256 = lo; b256 < hi; b256 += 256) {
-            const uint4 r = philox_block((uint32_t)(((b256 >> 8) << 6) | lane), c1, g0, g1, k0, k1);
-            for (int base = b256; base < min(hi, b256 + 256); base += 64) {
-                const int s = base + lane;
-                const bool valid = s < hi;
-                const uint32_t bk = valid ? pick4(r, (base >> 6) & 3) >> (32 - LOGK1) : 0u;
-                const uint64_t vmask = __ballot(valid);
-                uint64_t peers = vmask, mine = vmask;
-#pragma unroll
-                for (int bit = 0; bit < LOGK1; ++bit) {
-                    const uint64_t bal = __ballot(valid && ((bk >> bit) & 1u));
-                    peers &= ((bk >> bit) & 1u) ? bal : ~bal;
-                    mine &= ((lane >> bit) & 1) ? bal : ~bal;
-                }
-                if (scatter) {
-                    const int off = __shfl(reg, (int)bk, kWave);
-                    if (valid) L1[off + __popcll(peers & lt_mask)] = (uint16_t)(csr ? sh.vsock[s] : s / dv);
-                }
-                reg += __popcll(mine);
-            }
-        }
-    };
-    // level 1: counts -> offsets, bucket-major / wave-minor (thread b < K1 owns bucket b)
-    auto offsets1 = [&](int &start, int &size) {
-        size = 0;
-        if (tid < K1)
-            for (int w = 0; w < NW; ++w) size += cnt1[tid * NW + w];
-        int total = 0;
-        start = block_excl_scan(size, wsum, total);
-        if (tid < K1) {
-            int run = start;
-            for (int w = 0; w < NW; ++w) {
-                const int c = cnt1[tid * NW + w];
-                cnt1[tid * NW + w] = run;
-                run += c;
-            }
-        }
-        __syncthreads();
-    };
-    // level 2: thread tid owns buckets tid*BPT .. +BPT; their starts / sizes
-    auto offsets2 = [&](int (&st)[BPT], int (&sz)[BPT]) {
-        int size = 0;
-#pragma unroll
-        for (int j = 0; j < BPT; ++j) {
-            sz[j] = 0;
-            for (int w = 0; w < NW; ++w) sz[j] += cnt2[(tid * BPT + j) * NW + w];
-            size += sz[j];
-        }
-        int total = 0;
-        int run = block_excl_scan(size, wsum, total);
-#pragma unroll
-        for (int j = 0; j < BPT; ++j) {
-            st[j] = run;
-            for (int w = 0; w < NW; ++w) {
-                const int c = cnt2[(tid * BPT + j) * NW + w];
-                cnt2[(tid * BPT + j) * NW + w] = (uint16_t)run;
-                run += c;
-            }
-        }
+    int32_t *vl = variable_lookup + (size_t)blockIdx.x * E;
+    auto var_of = [&](int s) { return csr ? sh.vsock[s] : s / dv; };
+    auto clear_bm = [&](int words) {
+        uint4 *b4 = reinterpret_cast<uint4 *>(bm);
+        for (int w = lane; w < (words + 3) >> 2; w += kWave) b4[w] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
     };
 
     int att = 0;
     bool ok = false;
     while (!ok && att < max_attempts) {
-        const uint32_t ca = kSampleTag | ((uint32_t)att << 2);
-        // ---- level 1
-        int reg = 0;
-        pass1(ca | 2u, false, reg);
-        if (lane < K1) cnt1[lane * NW + wave] = reg;
-        __syncthreads();
-        int st1, sz1;
-        offsets1(st1, sz1);
-        if (tid < K1) sst[tid] = st1;
-        if (tid == 0) sst[K1] = E;
-        reg = lane < K1 ? cnt1[lane * NW + wave] : 0;
-        if (!(LDPC_SAMPLER_SKIP & 32)) pass1(ca | 2u, true, reg);
-        __threadfence_block();
-        __syncthreads();
-        // ---- level 2, super-bucket by super-bucket, validating finished checks
+        const uint32_t c1 = kSampleTag | ((uint32_t)att << 2) | 3u;
+        int R = E, x0 = 0, cdone = 0;
+        const int32_t *cur = nullptr;  // stage-0 pool: socket s -> var_of(s)
+        int32_t *nxt = vl;
         bool bad = false;
-        int done = 0;  // checks validated so far
-        for (int i = 0; i < ((LDPC_SAMPLER_SKIP & 16) ? 0 : (LDPC_SAMPLER_SKIP & 64) ? 1 : K1) && !bad; ++i) {
-            const int st = sst[i], S = sst[i + 1] - st;
-            if (S > kBigCap) {
-                bad = true;
-                break;
+        // checks whose slots all lie below `upto`, from cdone on: any repeated variable?
+        auto validate = [&](int upto) -> bool {
+            int cend = cdone;
+            if (csr) {
+                for (;;) {
+                    const int c = cend + lane;
+                    const uint64_t f = __ballot(c < m && sh.cptr[c + 1] <= upto);  // a prefix of the lanes
+                    cend += __popcll(f);
+                    if (f != ~0ull) break;
+                }
+            } else {
+                cend = upto / dc;
             }
-            const uint32_t ci = ca | ((uint32_t)i << 22);
-            for (int x = tid; x < S; x += T) A[x] = L1[st + x];
-            for (int x = tid; x < K2 * NW; x += T) cnt2[x] = 0;
-            __syncthreads();
-            pass(S, ci, LOGK2, [&](int, int bk, int rank, uint64_t peers) {
-                if (rank == 0) cnt2[bk * NW + wave] += (uint16_t)__popcll(peers);
-            });
-            __syncthreads();
-            int st2[BPT], sz2[BPT];
-            offsets2(st2, sz2);
-            pass(S, ci, LOGK2, [&](int s, int bk, int rank, uint64_t peers) {
-                Bf[cnt2[bk * NW + wave] + rank] = A[s];
-                if (rank == 0) cnt2[bk * NW + wave] += (uint16_t)__popcll(peers);
-            });
-            __syncthreads();
-            if (!(LDPC_SAMPLER_SKIP & 2)) {
+            bool b = false;
+            for (int cb = cdone; cb < cend; cb += kWave) {
+                const int c = cb + lane;
+                if (c < cend) {
+                    const int lo = csr ? sh.cptr[c] : c * dc, d = csr ? sh.cptr[c + 1] - lo : dc;
+                    if (d <= 8) {
+                        int v[8];
 #pragma unroll
-                for (int j = 0; j < BPT; ++j) {
-                    BucketRng rng{k0, k1, (uint32_t)(tid * BPT + j) << 20, ci | 1u, g0, g1};
-                    uint16_t *bb = Bf + st2[j];
-                    for (int x = sz2[j] - 1; x >= 1; --x) {
-                        const int jj = (int)rng.below((uint32_t)x + 1u);
-                        const uint16_t t = bb[x];
-                        bb[x] = bb[jj];
-                        bb[jj] = t;
+                        for (int a = 0; a < 8; ++a) v[a] = a < d ? ring[(lo + a) & (kSeqRing - 1)] : -1 - a;
+#pragma unroll
+                        for (int a = 0; a < 8; ++a)
+#pragma unroll
+                            for (int e = a + 1; e < 8; ++e) b |= v[a] == v[e];
+                    } else {
+                        for (int a = 0; a < d && !b; ++a) {
+                            const int va = ring[(lo + a) & (kSeqRing - 1)];
+                            for (int e = a + 1; e < d; ++e) b |= va == ring[(lo + e) & (kSeqRing - 1)];
+                        }
                     }
                 }
             }
-            __syncthreads();
-            for (int x = tid; x < S; x += T) out[st + x] = Bf[x];
+            cdone = cend;
+            return __ballot(b) == 0ull;
+        };
+
+        clear_bm((R + 31) >> 5);
+        while (R > kSeqFinal && !bad) {
+            const int Rn = (R + 3) >> 2, xend = E - Rn;
+            while (x0 < xend) {
+                const int x = x0 + lane;
+                const bool act = x < xend;
+                int i = 0;
+                bool exh = false;
+                if (act) {
+                    uint32_t kw = 0;
+                    uint4 blk = make_uint4(0u, 0u, 0u, 0u);
+                    auto next = [&](uint32_t &w) -> bool {
+                        if (kw >= 1024u) return false;
+                        if ((kw & 3u) == 0u) blk = philox_block((uint32_t)x | ((kw >> 2) << 24), c1, g0, g1, k0, k1);
+                        w = pick4(blk, (int)(kw & 3u));
+                        ++kw;
+                        return true;
+                    };
+                    for (;;) {
+                        uint32_t w;
+                        if (!next(w)) { exh = true; break; }
+                        uint64_t mm = (uint64_t)w * (uint32_t)R;
+                        uint32_t l = (uint32_t)mm;
+                        if (l < (uint32_t)R) {
+                            const uint32_t t = (0u - (uint32_t)R) % (uint32_t)R;
+                            while (l < t) {
+                                if (!next(w)) { exh = true; break; }
+                                mm = (uint64_t)w * (uint32_t)R;
+                                l = (uint32_t)mm;
+                            }
+                            if (exh) break;
+                        }
+                        i = (int)(mm >> 32);
+                        if (!((bm[i >> 5] >> (i & 31)) & 1u)) break;
+                    }
+                }
+                if (__ballot(exh)) { bad = true; break; }
+                const int val = act ? (cur ? cur[i] : var_of(i)) : 0;
+                const uint32_t bit = 1u << (i & 31);
+                bool dup = false;
+                if (act) dup = (atomicOr(&bm[i >> 5], bit) & bit) != 0u;
+                uint64_t dm = __ballot(dup);
+                int t = min(kWave, xend - x0);
+                if (dm) {
+                    // keep the lanes below the second-lowest lane of every group of equal picks
+                    while (dm) {
+                        const int p = (int)__builtin_ctzll(dm);
+                        const int ip = __shfl(i, p, kWave);
+                        const uint64_t grp = __ballot(act && i == ip);
+                        t = min(t, (int)__builtin_ctzll(grp & (grp - 1)));
+                        dm &= ~grp;
+                    }
+                    if (act && !dup) atomicAnd(&bm[i >> 5], ~bit);  // undo every pick of the round ...
+                    if (act && lane < t) atomicOr(&bm[i >> 5], bit);  // ... and redo the kept ones
+                }
+                if (lane < t) {
+                    out[x] = val;
+                    ring[x & (kSeqRing - 1)] = val;
+                }
+                x0 += t;
+                __syncthreads();
+                if (!validate(x0)) { bad = true; break; }
+            }
+            if (bad) break;
+            // compact the unused pool entries, in order, into the next pool
+            int32_t *dst = Rn <= kSeqFinal ? fin : nxt;
+            const int words = (R + 31) >> 5;
+            int base = 0;
+            for (int w0 = 0; w0 < words; w0 += kWave) {
+                const int w = w0 + lane;
+                uint32_t un = 0u;
+                if (w < words) {
+                    un = ~bm[w];
+                    const int valid = R - w * 32;
+                    if (valid < 32) un &= (1u << valid) - 1u;
+                }
+                int tot = 0;
+                int o = base + wave_excl_scan(__popc(un), tot);
+                while (un) {
+                    const int b = __ffs(un) - 1;
+                    un &= un - 1u;
+                    const int idx = w * 32 + b;
+                    dst[o++] = cur ? cur[idx] : var_of(idx);
+                }
+                base += tot;
+            }
             __threadfence_block();
             __syncthreads();
-            // checks whose slots all lie below st + S
-            int hi_c;
-            if (csr) {
-                int lo = done, hi = m;  // first c >= done with cptr[c+1] > st + S
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (sh.cptr[mid + 1] <= st + S) lo = mid + 1;
-                    else hi = mid;
+            if (dst != fin) {
+                cur = dst;
+                nxt = dst == vl ? vl + E / 2 : vl;
+            }
+            R = Rn;
+            clear_bm((R + 31) >> 5);
+        }
+        if (!bad) {
+            // last R <= kSeqFinal entries (in fin): Fisher-Yates by lane 0, then the last slots
+            if (R == E && lane < E) fin[lane] = var_of(lane);  // tiny graphs: no compaction ran
+            __syncthreads();
+            if (lane == 0) {
+                BucketRng rng{k0, k1, 0u, c1 | (1u << 30), g0, g1};
+                for (int a = R - 1; a >= 1; --a) {
+                    const int j = (int)rng.below((uint32_t)a + 1u);
+                    const int tmp = fin[a];
+                    fin[a] = fin[j];
+                    fin[j] = tmp;
                 }
-                hi_c = lo;
-            } else {
-                hi_c = (st + S) / dc;
             }
-            int b = 0;
-            for (int c = done + tid; c < hi_c; c += T) {
-                const int lo = csr ? sh.cptr[c] : c * dc, d = csr ? sh.cptr[c + 1] - lo : dc;
-                const int32_t *r = out + lo;
-                for (int x = 0; x < d && !b; ++x)
-                    for (int y = x + 1; y < d; ++y) b |= (r[x] == r[y]);
+            __syncthreads();
+            if (lane < R) {
+                const int x = x0 + lane;
+                out[x] = fin[lane];
+                ring[x & (kSeqRing - 1)] = fin[lane];
             }
-            done = hi_c;
-            bad = __syncthreads_or(b);
+            __syncthreads();
+            bad = !validate(E);
         }
         ok = !bad;
         ++att;
-        if (LDPC_SAMPLER_FIXED_ATT > 0) ok = att >= LDPC_SAMPLER_FIXED_ATT;
     }
-    if (attempts && tid == 0) attempts[blockIdx.x] = ok ? att : -att;
-    if (LDPC_SAMPLER_SKIP & 8) return;
-    sample_emit_var_side(sh, out, variable_lookup + (size_t)blockIdx.x * E);
+    if (attempts && lane == 0) attempts[blockIdx.x] = ok ? att : -att;
+    if (!ok)  // max_attempts without a simple graph: the identity configuration (in-range ids)
+        for (int x = lane; x < E; x += kWave) out[x] = var_of(x);
+    __threadfence_block();
+    __syncthreads();
+    if (fb == 0) {
+        sample_emit_var_side(sh, out, vl);
+        return;
+    }
+    // variable side: occurrence rank of each slot's variable from fb-bit LDS counters
+    // (slot order, so rows come out nearly ascending), then a per-row insertion sort
+    clear_bm(bw);
+    const uint32_t fmask = (1u << fb) - 1u;
+    for (int xb = 0; xb < E; xb += kWave) {
+        const int x = xb + lane;
+        if (x < E) {
+            const int v = out[x];
+            const uint32_t pos = (uint32_t)v * (uint32_t)fb;
+            const uint32_t old = atomicAdd(&bm[pos >> 5], 1u << (pos & 31));
+            const int rank = (int)((old >> (pos & 31)) & fmask);
+            if (csr) vl[sh.vptr[v] + rank] = x;
+            else vl[(size_t)v * dv + rank] = x / dc;
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int v = lane; v < n; v += kWave) {
+        int32_t *r = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
+        const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
+        for (int x = 1; x < deg; ++x) {
+            const int key = r[x];
+            int y = x - 1;
+            while (y >= 0 && r[y] > key) {
+                r[y + 1] = r[y];
+                --y;
+            }
+            r[y + 1] = key;
+        }
+    }
 }
 
 template <int T, typename Idx, bool LDSBUF>
@@ -2985,7 +3025,7 @@ __global__ __launch_bounds__(T) void sample_regular_kernel(SampleShape sh, uint3
         }
         __syncthreads();
         // 2. Fisher-Yates inside bucket `tid`
-        if (!(LDPC_SAMPLER_SKIP & 2)) {
+        {
             BucketRng rng{k0, k1, (uint32_t)tid << 20, c1 | 1u, g0, g1};
             Idx *bb = buf + start;
             for (int i = size - 1; i >= 1; --i) {
@@ -3006,16 +3046,10 @@ __global__ __launch_bounds__(T) void sample_regular_kernel(SampleShape sh, uint3
         }
         ok = !__syncthreads_or(bad);
         ++att;
-        if (LDPC_SAMPLER_FIXED_ATT > 0) ok = att >= LDPC_SAMPLER_FIXED_ATT;
     }
     if (attempts && tid == 0) attempts[blockIdx.x] = ok ? att : -att;
     // check_lookup (variable ids per slot); variable_lookup rows claimed by CAS, then sorted
     int32_t *vl = variable_lookup + (size_t)blockIdx.x * E;
-    if (LDPC_SAMPLER_SKIP & 8) {
-        if (LDPC_SAMPLER_FIXED_ATT > 0)
-            for (int x = tid; x < E; x += T) chk[x] = buf[x];
-        return;
-    }
     if (LDSBUF)
         for (int x = tid; x < E; x += T) chk[x] = buf[x];
     sample_emit_var_side(sh, chk, vl);
@@ -3923,9 +3957,9 @@ hipError_t launch_mc_decode(const ldpc_graph &g, int channel, float p, float p2,
     return dispatch_bp_algo<true>(g, a, algo, early_stop, stream);
 }
 
-static hipError_t launch_sample(const SampleShape &sh, uint64_t seed, uint64_t first_graph, int G,
-                                int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts, int max_attempts,
-                                hipStream_t stream) {
+static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vdeg, uint64_t seed,
+                                uint64_t first_graph, int G, int32_t *check_lookup, int32_t *variable_lookup,
+                                int32_t *attempts, int max_attempts, hipStream_t stream) {
     if (G <= 0) return hipSuccess;
     const int E = sh.E;
     const int K = sample_buckets(E);
@@ -3944,23 +3978,18 @@ static hipError_t launch_sample(const SampleShape &sh, uint64_t seed, uint64_t f
     } while (0)
     if (K == 256 && u16) LDPC_SAMPLE(256, uint16_t, true);
     if (K == 512 && u16) LDPC_SAMPLE(512, uint16_t, true);
-    const int logk1 = big_superbuckets_log2(E);
-    if (u16 && logk1 > 0) {
-        const size_t lds = (size_t)2 * kBigK2 * (kBigT / kWave) + (size_t)4 * ((1 << logk1) * (kBigT / kWave) + 16 + 68) +
-                           (size_t)4 * kBigCap;
-#define LDPC_BIG(L)                                                                                            \
-    case L: {                                                                                                  \
-        hipError_t e = allow_lds(sample_big_kernel<L>, lds);                                                   \
-        if (e != hipSuccess) return e;                                                                         \
-        hipLaunchKernelGGL(sample_big_kernel<L>, dim3(G), dim3(kBigT), lds, stream, sh, k0, k1, first_graph,   \
-                           check_lookup, variable_lookup, attempts, max_attempts);                             \
-        return hipGetLastError();                                                                              \
-    }
-        switch (logk1) {
-            LDPC_BIG(1) LDPC_BIG(2) LDPC_BIG(3) LDPC_BIG(4) LDPC_BIG(5) LDPC_BIG(6)
-            default: break;
-        }
-#undef LDPC_BIG
+    if (E >= kSeqMinE && E <= kSeqMaxE && max_cdeg <= kSeqMaxCdeg) {
+        // bitmap words (a multiple of 4: cleared with 16-byte stores); rank counters of
+        // fb bits per variable share them when they fit
+        int bw = ((E + 31) / 32 + 3) & ~3;
+        const int fb = max_vdeg <= 3 ? 2 : (max_vdeg <= 15 ? 4 : (max_vdeg <= 255 ? 8 : 0));
+        const int fbu = fb && (long)sh.n * fb <= (long)bw * 32 ? fb : 0;
+        const size_t lds = (size_t)4 * (bw + kSeqRing + kSeqFinal);
+        hipError_t e = allow_lds(sample_seq_kernel, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(sample_seq_kernel, dim3(G), dim3(kWave), lds, stream, sh, k0, k1, first_graph,
+                           check_lookup, variable_lookup, attempts, max_attempts, bw, fbu);
+        return hipGetLastError();
     }
     LDPC_SAMPLE(1024, int32_t, false);
 #undef LDPC_SAMPLE
@@ -3970,14 +3999,17 @@ hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t 
                                  int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts,
                                  int max_attempts, hipStream_t stream) {
     const SampleShape sh{n, n * dv / dc, n * dv, dv, dc, nullptr, nullptr, nullptr};
-    return launch_sample(sh, seed, first_graph, G, check_lookup, variable_lookup, attempts, max_attempts, stream);
+    return launch_sample(sh, dc, dv, seed, first_graph, G, check_lookup, variable_lookup, attempts, max_attempts,
+                         stream);
 }
 
 hipError_t launch_sample_csr(int n, int m, int E, const int32_t *d_vsock, const int32_t *d_cptr,
-                             const int32_t *d_vptr, uint64_t seed, uint64_t first_graph, int G, int32_t *check_var,
-                             int32_t *var_slot, int32_t *attempts, int max_attempts, hipStream_t stream) {
+                             const int32_t *d_vptr, int max_cdeg, int max_vdeg, uint64_t seed, uint64_t first_graph,
+                             int G, int32_t *check_var, int32_t *var_slot, int32_t *attempts, int max_attempts,
+                             hipStream_t stream) {
     const SampleShape sh{n, m, E, 0, 0, d_vsock, d_cptr, d_vptr};
-    return launch_sample(sh, seed, first_graph, G, check_var, var_slot, attempts, max_attempts, stream);
+    return launch_sample(sh, max_cdeg, max_vdeg, seed, first_graph, G, check_var, var_slot, attempts, max_attempts,
+                         stream);
 }
 
 hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,

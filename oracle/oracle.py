@@ -57,6 +57,8 @@ def lib():
         _lib.oracle_sample_regular_batch.restype = None
         _lib.oracle_sample_csr.argtypes = [i, i, P, P, u64, u64, i, P, P]
         _lib.oracle_sample_csr.restype = i
+        _lib.oracle_sampler_force_seq.argtypes = [i]
+        _lib.oracle_sampler_force_seq.restype = None
         _lib.oracle_check_update.argtypes = [P, i, i, f]
         _lib.oracle_check_update.restype = None
         _lib.oracle_num_threads.argtypes = []
@@ -182,6 +184,12 @@ def sample_regular_batch(n, dv, dc, seed, first_graph, G, max_attempts=1 << 20):
     att = np.zeros(G, np.int32)
     lib().oracle_sample_regular_batch(n, dv, dc, seed, first_graph, G, max_attempts, _p(chk), _p(var), _p(att))
     return chk, var, att
+
+
+def sampler_force_seq(on):
+    """Tests only: restate the sequential-draw sampler (sample_seq_kernel) at every graph
+    size instead of the kernels' size rule."""
+    lib().oracle_sampler_force_seq(1 if on else 0)
 
 
 def sample_csr(var_ptr, check_ptr, seed, graph, max_attempts=1 << 20):

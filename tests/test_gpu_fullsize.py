@@ -132,7 +132,7 @@ def test_cfg5_ensemble_mc_n64800_vs_oracle(torch):
     """configs[4]: 64 trials on 64 fresh n = 64,800 graphs, 200 iterations, X = 3, run as
     two 32-trial batches (trial index = graph index = channel subsequence)."""
     from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
-    n, iters, eps, seed, X, B = 64800, 200, 0.425, 23, 3, 32
+    n, iters, eps, seed, X, B = 64800, 200, 0.427, 23, 3, 32
     mc = MonteCarlo.ensemble(n, 3, 6, "bec", eps, iters, seed=seed, batch=B, expurgation=X)
     mc.run_batch(0, B)
     mc.run_batch(B, B)
@@ -153,5 +153,5 @@ def test_cfg5_ensemble_mc_n64800_vs_oracle(torch):
         want[3] += it
     _dump("cfg5_ensemble_mc", {"trials": int(want[0]), "frame_errors": int(want[1]),
                                "mean_iterations": float(want[3] / want[0])})
-    assert 0 < want[1] < T  # both decoded and failed trials at eps = 0.425 (threshold 0.4294)
+    assert 0 < want[1] < T  # both decoded and failed trials at eps = 0.427 (threshold 0.4294; 10 of 64 with these graphs)
     np.testing.assert_array_equal(got, want)

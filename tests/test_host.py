@@ -219,6 +219,62 @@ def test_oracle_sampler_attempts_geometric():
     assert np.all(a > 0) and 90 < a.mean() < 250
 
 
+@pytest.fixture
+def force_seq():
+    oracle.sampler_force_seq(True)
+    yield
+    oracle.sampler_force_seq(False)
+
+
+def test_oracle_seq_sampler_law_matches_reference_generator(force_seq):
+    """The sequential-draw form (sample_seq_kernel, n*dv >= 65536 on the device) forced onto
+    small graphs: simple graphs, consistent lists and the reference generator's 4-cycle
+    statistic (random_code_generator.c:21-67), at n = 40 (one final Fisher-Yates stage) and
+    n = 400 (two compaction stages before it)."""
+    if not oracle.ref_available():
+        pytest.skip("oracle/_ref not built")
+
+    def c4(chk, n, m):
+        H = np.zeros((m, n), np.int64)
+        for c in range(m):
+            H[c, chk[c * 6:(c + 1) * 6]] = 1
+        O = H @ H.T
+        np.fill_diagonal(O, 0)
+        return int((O * (O - 1) // 2).sum() // 2)
+
+    for n, N in ((40, 300), (400, 300)):
+        m = n // 2
+        ref = [c4(oracle.ref_generate_random_code(n, 3, 6)[0], n, m) for _ in range(N)]
+        ours, atts = [], []
+        for gid in range(N):
+            chk, var, att = oracle.sample_regular(n, 3, 6, 12, gid)
+            assert att > 0
+            rows = chk.reshape(m, 6)
+            assert all(len(set(r)) == 6 for r in rows)
+            v = var.reshape(n, 3)
+            assert np.all(np.diff(v, axis=1) > 0)
+            assert np.array_equal(np.sort(chk), np.repeat(np.arange(n), 3))
+            ours.append(c4(chk, n, m))
+            atts.append(att)
+        assert abs(np.mean(ref) - np.mean(ours)) < 4 * np.sqrt((np.var(ref) + np.var(ours)) / N), (n, np.mean(ref),
+                                                                                                  np.mean(ours))
+        if n == 400:  # whole-graph redraw: attempts ~ Geometric(P(simple)), P ~ exp(-5) for (3,6)
+            assert 60 < np.mean(atts) < 250
+
+
+def test_oracle_seq_sampler_full_size():
+    """configs[4]'s n = 64,800 takes the sequential-draw form by the size rule: simple graph,
+    every variable three times, sorted variable rows; deterministic per graph id."""
+    chk, var, att = oracle.sample_regular(64800, 3, 6, 5, 9)
+    assert att > 0
+    assert np.all(np.diff(np.sort(chk.reshape(-1, 6), axis=1), axis=1) > 0)
+    assert np.array_equal(np.bincount(chk, minlength=64800), np.full(64800, 3))
+    v = var.reshape(-1, 3)
+    assert np.all(np.diff(v, axis=1) > 0)
+    chk2, _, att2 = oracle.sample_regular(64800, 3, 6, 5, 9)
+    assert att2 == att and np.array_equal(chk, chk2)
+
+
 @pytest.mark.parametrize("kind", ["rsu20000", "rsu2000", "csr36"])
 def test_irregular_layout_invariants(kind):
     """bp_irr_kernel's host layout (build_irr_layout): every CSR edge gets the position of its
