@@ -2698,6 +2698,15 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
 // oracle_sample_regular / oracle_sample_csr restate it bit for bit.
 constexpr int kSeqFinal = 64, kSeqRing = 256;
 
+// LDS ordering between the lanes of one wave (LDS instructions of a wave execute in order):
+// a compiler barrier only -- no s_barrier, no wait for the outstanding global stores that a
+// workgroup-scope fence (__syncthreads) would add to every round
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ int wave_excl_scan(int v, int &total) {
     const int lane = threadIdx.x & 63;
     int incl = v;
@@ -2713,7 +2722,7 @@ __device__ __forceinline__ int wave_excl_scan(int v, int &total) {
 __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
                                                            uint64_t first_graph, int32_t *check_lookup,
                                                            int32_t *variable_lookup, int32_t *attempts,
-                                                           int max_attempts, int bw, int fb) {
+                                                           int max_attempts, int bw, int fb, uint32_t mdv) {
     extern __shared__ __align__(16) unsigned char smem[];
     uint32_t *bm = reinterpret_cast<uint32_t *>(smem);  // [bw] pool bitmap, later rank counters
     int *ring = reinterpret_cast<int *>(bm + bw);       // [kSeqRing] variable of slot x at x % kSeqRing
@@ -2725,11 +2734,15 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
     const uint32_t g0 = (uint32_t)gid, g1 = (uint32_t)(gid >> 32);
     int32_t *out = check_lookup + (size_t)blockIdx.x * E;
     int32_t *vl = variable_lookup + (size_t)blockIdx.x * E;
-    auto var_of = [&](int s) { return csr ? sh.vsock[s] : s / dv; };
+    // socket -> variable; regular: s / dv as a multiply-high by mdv = ceil(2^32 / dv) (exact for
+    // s < 2^24, dv < 256; mdv = 0: divide)
+    auto var_of = [&](int s) {
+        return csr ? sh.vsock[s] : (mdv ? (int)__umulhi((uint32_t)s, mdv) : s / dv);
+    };
     auto clear_bm = [&](int words) {
         uint4 *b4 = reinterpret_cast<uint4 *>(bm);
         for (int w = lane; w < (words + 3) >> 2; w += kWave) b4[w] = make_uint4(0u, 0u, 0u, 0u);
-        __syncthreads();
+        wave_sync();
     };
 
     int att = 0;
@@ -2838,7 +2851,7 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
                     ring[x & (kSeqRing - 1)] = val;
                 }
                 x0 += t;
-                __syncthreads();
+                wave_sync();
                 if (!validate(x0)) { bad = true; break; }
             }
             if (bad) break;
@@ -2876,7 +2889,7 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
         if (!bad) {
             // last R <= kSeqFinal entries (in fin): Fisher-Yates by lane 0, then the last slots
             if (R == E && lane < E) fin[lane] = var_of(lane);  // tiny graphs: no compaction ran
-            __syncthreads();
+            wave_sync();
             if (lane == 0) {
                 BucketRng rng{k0, k1, 0u, c1 | (1u << 30), g0, g1};
                 for (int a = R - 1; a >= 1; --a) {
@@ -2886,13 +2899,13 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
                     fin[j] = tmp;
                 }
             }
-            __syncthreads();
+            wave_sync();
             if (lane < R) {
                 const int x = x0 + lane;
                 out[x] = fin[lane];
                 ring[x & (kSeqRing - 1)] = fin[lane];
             }
-            __syncthreads();
+            wave_sync();
             bad = !validate(E);
         }
         ok = !bad;
@@ -3987,8 +4000,10 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
         const size_t lds = (size_t)4 * (bw + kSeqRing + kSeqFinal);
         hipError_t e = allow_lds(sample_seq_kernel, lds);
         if (e != hipSuccess) return e;
+        const uint32_t mdv =
+            sh.vsock == nullptr && sh.dv > 1 && sh.dv < 256 ? (uint32_t)((0x100000000ull + sh.dv - 1) / sh.dv) : 0u;
         hipLaunchKernelGGL(sample_seq_kernel, dim3(G), dim3(kWave), lds, stream, sh, k0, k1, first_graph,
-                           check_lookup, variable_lookup, attempts, max_attempts, bw, fbu);
+                           check_lookup, variable_lookup, attempts, max_attempts, bw, fbu, mdv);
         return hipGetLastError();
     }
     LDPC_SAMPLE(1024, int32_t, false);
