@@ -2675,19 +2675,21 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
 // being simple -- drawn slot by slot, so a bad check is seen as soon as its last
 // slot is drawn and the attempt stops there (a failing (3,6) attempt at n = 64,800
 // stops after ~1/5 of the graph instead of paying a whole permutation):
-//   * slot x (in order) takes a uniform unused entry of the pool: words of the
-//     Philox stream ctr {x | blk<<24, tag|att<<2|3, g_lo, g_hi} give Lemire draws
-//     on [0, R) until one lands on an unused pool index (a bitmap in LDS);
-//     1024 words without one reject the attempt (probability < (3/4)^1000);
+//   * slot x (in order) takes a uniform unused entry of the pool: its words --
+//     word j = word x&3 of Philox ctr {x>>2 | j<<20, tag|att<<2|3, g_lo, g_hi} --
+//     give Lemire draws on [0, R) until one lands on an unused pool index (a
+//     bitmap in LDS); 1024 words without one reject the attempt (probability
+//     < (3/4)^1000);
 //   * the pool starts as all R = E sockets; when R' = ceil(R/4) entries are left
 //     the unused ones are compacted in order into a new pool (global scratch,
 //     the variable_lookup row) with a fresh bitmap, so no draw ever sees more
 //     than 3/4 of its pool used; the last <= kSeqFinal entries are
 //     Fisher-Yates-shuffled by one lane (stream {blk, tag|1<<30|att<<2|3, g});
-//   * 64 consecutive slots are drawn per round, one per lane, against the bitmap
-//     of the slots before the round; an LDS atomic OR marks the picks, and when
-//     two lanes picked the same entry the round keeps only the lanes below the
-//     second-lowest lane of every such group (the later lanes redraw next round
+//   * up to 256 consecutive slots are drawn per round, the four of block x>>2 by
+//     one lane (one Philox block per lane per word index), against the bitmap of
+//     the slots before the round; LDS atomic ORs mark the picks, and when two
+//     slots picked the same entry the round keeps only the slots below the
+//     second-lowest slot of every such group (the later slots redraw next round
 //     from the updated bitmap -- a slot's result is its first draw not used by an
 //     earlier slot, exactly the sequential process);
 //   * every check whose slots are all drawn is tested (variable ids kept in an
@@ -2696,15 +2698,14 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
 // The variable side is built with per-variable occurrence counters packed fb bits
 // per variable into the bitmap's LDS (fb = 0: global CAS, sample_emit_var_side).
 // oracle_sample_regular / oracle_sample_csr restate it bit for bit.
-constexpr int kSeqFinal = 64, kSeqRing = 256;
+constexpr int kSeqFinal = 64, kSeqRing = 512;  // ring: a round (256 slots) + the check it completes
 
 // LDS ordering between the lanes of one wave (LDS instructions of a wave execute in order):
 // a compiler barrier only -- no s_barrier, no wait for the outstanding global stores that a
 // workgroup-scope fence (__syncthreads) would add to every round
 __device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    asm volatile("" ::: "memory");
 }
 
 __device__ __forceinline__ int wave_excl_scan(int v, int &total) {
@@ -2719,6 +2720,7 @@ __device__ __forceinline__ int wave_excl_scan(int v, int &total) {
     return incl - v;
 }
 
+template <bool CSR>  // CSR: irregular degree structure (sh.vsock / cptr / vptr)
 __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
                                                            uint64_t first_graph, int32_t *check_lookup,
                                                            int32_t *variable_lookup, int32_t *attempts,
@@ -2728,7 +2730,7 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
     int *ring = reinterpret_cast<int *>(bm + bw);       // [kSeqRing] variable of slot x at x % kSeqRing
     int *fin = ring + kSeqRing;                         // [kSeqFinal] last pool entries
     const int n = sh.n, E = sh.E, m = sh.m, dv = sh.dv, dc = sh.dc;
-    const bool csr = sh.vsock != nullptr;
+    constexpr bool csr = CSR;  // compile-time: the regular form has no global load in its stage-0 rounds
     const int lane = threadIdx.x;
     const uint64_t gid = first_graph + blockIdx.x;
     const uint32_t g0 = (uint32_t)gid, g1 = (uint32_t)(gid >> 32);
@@ -2750,13 +2752,11 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
     while (!ok && att < max_attempts) {
         const uint32_t c1 = kSampleTag | ((uint32_t)att << 2) | 3u;
         int R = E, x0 = 0, cdone = 0;
-        const int32_t *cur = nullptr;  // stage-0 pool: socket s -> var_of(s)
-        int32_t *nxt = vl;
         bool bad = false;
         // checks whose slots all lie below `upto`, from cdone on: any repeated variable?
         auto validate = [&](int upto) -> bool {
             int cend = cdone;
-            if (csr) {
+            if constexpr (csr) {
                 for (;;) {
                     const int c = cend + lane;
                     const uint64_t f = __ballot(c < m && sh.cptr[c + 1] <= upto);  // a prefix of the lanes
@@ -2791,72 +2791,110 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
             return __ballot(b) == 0ull;
         };
 
-        clear_bm((R + 31) >> 5);
-        while (R > kSeqFinal && !bad) {
-            const int Rn = (R + 3) >> 2, xend = E - Rn;
+        // the rounds of one stage (slots x0 .. xend - 1); POOL: the pool is the global row at
+        // vl + cur (stage 0: the sockets themselves -- the regular form has no global load in
+        // its rounds, so no round waits on the previous rounds' stores)
+        auto rounds = [&](auto pool_tag, int xend, int cur) {
+            constexpr bool POOL = decltype(pool_tag)::value;
+            const int32_t *pool = vl + cur;
+            const uint32_t lt = (0u - (uint32_t)R) % (uint32_t)R;  // Lemire: reject low words below this
             while (x0 < xend) {
-                const int x = x0 + lane;
-                const bool act = x < xend;
-                int i = 0;
+                // lane L: slots 4bb .. 4bb+3 of block bb = x0/4 + L (slots below x0 are done).
+                // Word j of slot x is word x&3 of Philox {x>>2 | j<<20, c1, g}: one block per lane
+                // per word index serves its four slots.  A word is rejected by Lemire's test or
+                // when its entry is used; every slot still looking takes its next word.
+                const int base = x0 & ~3;
+                const uint32_t bb = (uint32_t)(base >> 2) + (uint32_t)lane;
+                int i[4], val[4];
+                bool act[4], need[4], dup[4];
                 bool exh = false;
-                if (act) {
-                    uint32_t kw = 0;
-                    uint4 blk = make_uint4(0u, 0u, 0u, 0u);
-                    auto next = [&](uint32_t &w) -> bool {
-                        if (kw >= 1024u) return false;
-                        if ((kw & 3u) == 0u) blk = philox_block((uint32_t)x | ((kw >> 2) << 24), c1, g0, g1, k0, k1);
-                        w = pick4(blk, (int)(kw & 3u));
-                        ++kw;
-                        return true;
-                    };
-                    for (;;) {
-                        uint32_t w;
-                        if (!next(w)) { exh = true; break; }
-                        uint64_t mm = (uint64_t)w * (uint32_t)R;
-                        uint32_t l = (uint32_t)mm;
-                        if (l < (uint32_t)R) {
-                            const uint32_t t = (0u - (uint32_t)R) % (uint32_t)R;
-                            while (l < t) {
-                                if (!next(w)) { exh = true; break; }
-                                mm = (uint64_t)w * (uint32_t)R;
-                                l = (uint32_t)mm;
-                            }
-                            if (exh) break;
+                uint4 W = philox_block(bb, c1, g0, g1, k0, k1);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int x = base + 4 * lane + q;
+                    act[q] = x >= x0 && x < xend;
+                    const uint64_t mm = (uint64_t)pick4(W, q) * (uint32_t)R;
+                    i[q] = (int)(mm >> 32);
+                    need[q] = act[q] && ((uint32_t)mm < lt || ((bm[i[q] >> 5] >> (i[q] & 31)) & 1u));
+                }
+                for (uint32_t j = 1; __ballot(need[0] || need[1] || need[2] || need[3]); ++j) {
+                    if (j >= 1024u) {  // some slot rejected 1024 words: the attempt is rejected
+                        exh = true;
+                        break;
+                    }
+                    W = philox_block(bb | (j << 20), c1, g0, g1, k0, k1);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (need[q]) {
+                            const uint64_t mm = (uint64_t)pick4(W, q) * (uint32_t)R;
+                            i[q] = (int)(mm >> 32);
+                            need[q] = (uint32_t)mm < lt || ((bm[i[q] >> 5] >> (i[q] & 31)) & 1u);
                         }
-                        i = (int)(mm >> 32);
-                        if (!((bm[i >> 5] >> (i & 31)) & 1u)) break;
                     }
                 }
-                if (__ballot(exh)) { bad = true; break; }
-                const int val = act ? (cur ? cur[i] : var_of(i)) : 0;
-                const uint32_t bit = 1u << (i & 31);
-                bool dup = false;
-                if (act) dup = (atomicOr(&bm[i >> 5], bit) & bit) != 0u;
-                uint64_t dm = __ballot(dup);
-                int t = min(kWave, xend - x0);
-                if (dm) {
-                    // keep the lanes below the second-lowest lane of every group of equal picks
-                    while (dm) {
-                        const int p = (int)__builtin_ctzll(dm);
-                        const int ip = __shfl(i, p, kWave);
-                        const uint64_t grp = __ballot(act && i == ip);
-                        t = min(t, (int)__builtin_ctzll(grp & (grp - 1)));
-                        dm &= ~grp;
+                if (__ballot(exh)) { bad = true; return; }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    val[q] = 0;
+                    if (act[q]) val[q] = POOL ? pool[i[q]] : var_of(i[q]);
+                }
+                bool anyd = false;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t bit = 1u << (i[q] & 31);
+                    dup[q] = act[q] && (atomicOr(&bm[i[q] >> 5], bit) & bit) != 0u;
+                    anyd |= dup[q];
+                }
+                int t = min(4 * kWave, xend - base);  // kept: slots base + [x0 - base, t)
+                if (__ballot(anyd)) {
+                    // keep the slots below the second-lowest slot of every group of equal picks
+                    uint64_t dm[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) dm[q] = __ballot(dup[q]);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        while (dm[q]) {
+                            const int ip = __shfl(i[q], (int)__builtin_ctzll(dm[q]), kWave);
+                            int lo1 = 1 << 30, lo2 = 1 << 30;  // the group's two lowest slots
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const uint64_t g = __ballot(act[r] && i[r] == ip);
+                                dm[r] &= ~g;
+                                if (g) {
+                                    const int s1 = 4 * (int)__builtin_ctzll(g) + r;
+                                    const uint64_t g2 = g & (g - 1);
+                                    const int s2 = g2 ? 4 * (int)__builtin_ctzll(g2) + r : 1 << 30;
+                                    if (s1 < lo1) { lo2 = min(lo1, s2); lo1 = s1; }
+                                    else lo2 = min(lo2, s1);
+                                }
+                            }
+                            t = min(t, lo2);
+                        }
                     }
-                    if (act && !dup) atomicAnd(&bm[i >> 5], ~bit);  // undo every pick of the round ...
-                    if (act && lane < t) atomicOr(&bm[i >> 5], bit);  // ... and redo the kept ones
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)  // undo every pick of the round ...
+                        if (act[q] && !dup[q]) atomicAnd(&bm[i[q] >> 5], ~(1u << (i[q] & 31)));
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)  // ... and redo the kept ones
+                        if (act[q] && 4 * lane + q < t) atomicOr(&bm[i[q] >> 5], 1u << (i[q] & 31));
                 }
-                if (lane < t) {
-                    out[x] = val;
-                    ring[x & (kSeqRing - 1)] = val;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int x = base + 4 * lane + q;
+                    if (act[q] && 4 * lane + q < t) {
+                        out[x] = val[q];
+                        ring[x & (kSeqRing - 1)] = val[q];
+                    }
                 }
-                x0 += t;
+                x0 = base + t;
                 wave_sync();
-                if (!validate(x0)) { bad = true; break; }
+                if (!validate(x0)) { bad = true; return; }
             }
-            if (bad) break;
-            // compact the unused pool entries, in order, into the next pool
-            int32_t *dst = Rn <= kSeqFinal ? fin : nxt;
+        };
+        // compact the unused entries of the stage's pool (R entries), in order, into dst
+        auto compact = [&](auto pool_tag, int cur, auto *dst) {
+            constexpr bool POOL = decltype(pool_tag)::value;
+            const int32_t *pool = vl + cur;
             const int words = (R + 31) >> 5;
             int base = 0;
             for (int w0 = 0; w0 < words; w0 += kWave) {
@@ -2873,16 +2911,30 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
                     const int b = __ffs(un) - 1;
                     un &= un - 1u;
                     const int idx = w * 32 + b;
-                    dst[o++] = cur ? cur[idx] : var_of(idx);
+                    dst[o++] = POOL ? pool[idx] : var_of(idx);
                 }
                 base += tot;
             }
+        };
+
+        clear_bm((R + 31) >> 5);
+        int cur = -1;  // offset of the current pool in vl (-1: stage 0, the sockets)
+        while (R > kSeqFinal && !bad) {
+            const int Rn = (R + 3) >> 2, xend = E - Rn;
+            if (cur < 0) rounds(bool_c<false>{}, xend, 0);
+            else rounds(bool_c<true>{}, xend, cur);
+            if (bad) break;
+            if (Rn <= kSeqFinal) {  // the last entries go to LDS
+                if (cur < 0) compact(bool_c<false>{}, 0, fin);
+                else compact(bool_c<true>{}, cur, fin);
+            } else {  // the next pool: vl[0 ..) and vl[E/2 ..) alternately (R' <= E/4 + 1)
+                const int nx = cur == 0 ? E / 2 : 0;
+                if (cur < 0) compact(bool_c<false>{}, 0, vl + nx);
+                else compact(bool_c<true>{}, cur, vl + nx);
+                cur = nx;
+            }
             __threadfence_block();
             __syncthreads();
-            if (dst != fin) {
-                cur = dst;
-                nxt = dst == vl ? vl + E / 2 : vl;
-            }
             R = Rn;
             clear_bm((R + 31) >> 5);
         }
@@ -3998,11 +4050,12 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
         const int fb = max_vdeg <= 3 ? 2 : (max_vdeg <= 15 ? 4 : (max_vdeg <= 255 ? 8 : 0));
         const int fbu = fb && (long)sh.n * fb <= (long)bw * 32 ? fb : 0;
         const size_t lds = (size_t)4 * (bw + kSeqRing + kSeqFinal);
-        hipError_t e = allow_lds(sample_seq_kernel, lds);
+        auto kern = sh.vsock ? sample_seq_kernel<true> : sample_seq_kernel<false>;
+        hipError_t e = allow_lds(kern, lds);
         if (e != hipSuccess) return e;
         const uint32_t mdv =
             sh.vsock == nullptr && sh.dv > 1 && sh.dv < 256 ? (uint32_t)((0x100000000ull + sh.dv - 1) / sh.dv) : 0u;
-        hipLaunchKernelGGL(sample_seq_kernel, dim3(G), dim3(kWave), lds, stream, sh, k0, k1, first_graph,
+        hipLaunchKernelGGL(kern, dim3(G), dim3(kWave), lds, stream, sh, k0, k1, first_graph,
                            check_lookup, variable_lookup, attempts, max_attempts, bw, fbu, mdv);
         return hipGetLastError();
     }
