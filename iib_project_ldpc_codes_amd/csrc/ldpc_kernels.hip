@@ -10,6 +10,7 @@
 #include <rocrand/rocrand_kernel.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "ldpc_internal.hpp"
@@ -4041,9 +4042,12 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
                            variable_lookup, attempts, max_attempts);                                           \
         return hipGetLastError();                                                                              \
     } while (0)
-    if (K == 256 && u16) LDPC_SAMPLE(256, uint16_t, true);
-    if (K == 512 && u16) LDPC_SAMPLE(512, uint16_t, true);
-    if (E >= kSeqMinE && E <= kSeqMaxE && max_cdeg <= kSeqMaxCdeg) {
+    // LDPC_SEQ_MIN_E: timing experiments only (the oracle follows kSeqMinE)
+    static const int seq_min = getenv("LDPC_SEQ_MIN_E") ? atoi(getenv("LDPC_SEQ_MIN_E")) : kSeqMinE;
+    const bool seq = E >= seq_min && E <= kSeqMaxE && max_cdeg <= kSeqMaxCdeg;
+    if (K == 256 && u16 && !seq) LDPC_SAMPLE(256, uint16_t, true);
+    if (K == 512 && u16 && !seq) LDPC_SAMPLE(512, uint16_t, true);
+    if (seq) {
         // bitmap words (a multiple of 4: cleared with 16-byte stores); rank counters of
         // fb bits per variable share them when they fit
         int bw = ((E + 31) / 32 + 3) & ~3;
