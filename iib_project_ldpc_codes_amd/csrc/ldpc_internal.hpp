@@ -178,7 +178,7 @@ inline int sample_buckets(int E) { return E <= 16384 ? 256 : (E < 65536 ? 512 : 
 // Sequential-draw sampler (sample_seq_kernel, one wave per graph) for
 // kSeqMinE <= n*dv <= kSeqMaxE with check degrees <= kSeqMaxCdeg; the oracle's
 // SEQ_* constants must equal these.  Larger graphs: one level, K = 1024.
-constexpr int kSeqMinE = 65536, kSeqMaxE = 393216, kSeqMaxCdeg = 192;
+constexpr int kSeqMinE = 8192, kSeqMaxE = 393216, kSeqMaxCdeg = 192;
 
 // Random regular graphs on the device (law of random_code_generator.c), one
 // workgroup per graph; attempts[g] = number of permutations drawn (negative if

@@ -2671,7 +2671,7 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
     }
 }
 
-// Large graphs (65536 <= n*dv <= kSeqMaxE): sequential-draw sampler, one wave per
+// Graphs with kSeqMinE (8192) <= n*dv <= kSeqMaxE: sequential-draw sampler, one wave per
 // graph.  The same law -- a uniform socket permutation conditioned on every check
 // being simple -- drawn slot by slot, so a bad check is seen as soon as its last
 // slot is drawn and the attempt stops there (a failing (3,6) attempt at n = 64,800

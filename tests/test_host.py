@@ -227,7 +227,7 @@ def force_seq():
 
 
 def test_oracle_seq_sampler_law_matches_reference_generator(force_seq):
-    """The sequential-draw form (sample_seq_kernel, n*dv >= 65536 on the device) forced onto
+    """The sequential-draw form (sample_seq_kernel, n*dv >= 8192 on the device) forced onto
     small graphs: simple graphs, consistent lists and the reference generator's 4-cycle
     statistic (random_code_generator.c:21-67), at n = 40 (one final Fisher-Yates stage) and
     n = 400 (two compaction stages before it)."""
