@@ -44,9 +44,6 @@ constexpr int kWave = 64;
 #ifndef LDPC_BEC_DEC_BITS
 #define LDPC_BEC_DEC_BITS 1  // batch BEC decode (B >= 64) on the bit-sliced kernel when its planes fit LDS
 #endif
-#ifndef LDPC_ABLATE_CHECK
-#define LDPC_ABLATE_CHECK 0
-#endif
 #ifndef LDPC_SPA_RWIRE
 #define LDPC_SPA_RWIRE 1  // bp_lds_kernel sum-product: v->c wire = the clamped ratio R itself (see ratio_wire)
 #endif
@@ -61,12 +58,6 @@ constexpr int kWave = 64;
 #endif
 #ifndef LDPC_CHECK_W64
 #define LDPC_CHECK_W64 0  // check phase writes each pair edge with its own ds_write_b64
-#endif
-#ifndef LDPC_ABLATE_VARIO
-#define LDPC_ABLATE_VARIO 0  // timing ablation only: 1 = no variable-phase stores, 2 = no gathers
-#endif
-#ifndef LDPC_ABLATE_BARRIER
-#define LDPC_ABLATE_BARRIER 0  // timing ablation only: 1 = drop the two per-iteration barriers (racy)
 #endif
 #ifndef LDPC_ABLATE_PHASE
 #define LDPC_ABLATE_PHASE 0    // timing ablation only: 1 = skip the check phase, 2 = skip the variable phase
@@ -1221,7 +1212,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     a1[j] = addr(i + 1, j);
                 }
 #pragma unroll
-                for (int j = 0; j < DV; ++j) if (LDPC_ABLATE_VARIO != 2) cv[j] = make_float2(at(a0[j]), at(a1[j]));
+                for (int j = 0; j < DV; ++j) cv[j] = make_float2(at(a0[j]), at(a1[j]));
                 if constexpr (FINAL) {
                     float2 s = make_float2(llr_log2(i), llr_log2(i + 1));
 #pragma unroll
@@ -1229,21 +1220,10 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                         s = s + make_float2(__builtin_amdgcn_logf(cv[j].x), __builtin_amdgcn_logf(cv[j].y));
                     if constexpr (!MC) { pr[i] = s.x; pr[i + 1] = s.y; }
                 } else {
-                    if constexpr (LDPC_ABLATE_VARIO == 2) {
-#pragma unroll
-                        for (int j = 0; j < DV; ++j) {
-                            cv[j] = make_float2(__uint_as_float(a0[j]) , __uint_as_float(a1[j]));
-                            asm volatile("" : "+v"(cv[j].x), "+v"(cv[j].y));
-                        }
-                    }
                     const float2 post = edges(cv, make_float2(L[i], L[i + 1]), [&](int j, float2 R) {
                         const float2 w = ratio_wire2(R);
-                        if constexpr (LDPC_ABLATE_VARIO == 1) {
-                            asm volatile("" :: "v"(w.x), "v"(w.y));
-                        } else {
-                            at(a0[j]) = w.x;
-                            at(a1[j]) = w.y;
-                        }
+                        at(a0[j]) = w.x;
+                        at(a1[j]) = w.y;
                     });
                     if constexpr (ET) {
                         put_hard(i, post.x < 1.0f, a0);
@@ -1360,7 +1340,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 
         int it = 0;
         for (; it < iters; ++it) {
-            if (it > 0 && !LDPC_ABLATE_BARRIER) __syncthreads();  // variable phase (msg, hs) complete
+            if (it > 0) __syncthreads();  // variable phase (msg, hs) complete
             // check phase; with ET it also evaluates the syndrome of the previous
             // iteration's hard decisions, and the decoder stops before the next
             // variable phase when every check is satisfied
@@ -1380,10 +1360,6 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                 float2 x2[DC];
 #pragma unroll
                 for (int i = 0; i < DC; ++i) x2[i] = pp[i];
-#if LDPC_ABLATE_CHECK
-#pragma unroll
-                for (int i = 0; i < DC; ++i) x2[i] = x2[i] * make_float2(0.5f, 0.5f);  // timing ablation only
-#else
                 if constexpr (ALGO == 0) {
                     if constexpr (LDPC_SPA_RWIRE && PROD) check_update_spa_pair_rwire<DC>(x2);
                     else check_update_spa_pair<DC, !PROD>(x2);
@@ -1401,7 +1377,6 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 #pragma unroll
                     for (int i = 0; i < DC; ++i) x2[i] = make_float2(xa[i], xb[i]);
                 }
-#endif
 #pragma unroll
                 for (int i = 0; i < DC; ++i) {
                     if constexpr (LDPC_CHECK_W64) {
@@ -1418,7 +1393,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             }
             if constexpr (ET) {
                 if (!__syncthreads_or(unsat | (it == 0))) break;
-            } else if (!LDPC_ABLATE_BARRIER) {
+            } else {
                 __syncthreads();
             }
             // fixed-count decode: the last variable phase runs after the loop
