@@ -521,6 +521,22 @@ def main():
         extras["bsc_minsum_mc_cfg2_p0.07_early_stop"] = {
             "trials_per_s": Bm / (a.elapsed_time(b) * 1e-3), "batch": Bm, "mean_iterations": float(cnt[3] / cnt[0]),
             "fer": float(cnt[1] / cnt[0])}
+        # configs[4] shape: expurgated (3,6) ensemble, a fresh device-sampled n = 64,800 graph per
+        # trial (sample_seq_kernel) + 200-iteration BEC decode + counters, eps = 0.42, X = 3
+        # (parallel_simulator_expurgated.py:169-285)
+        Be = 16384
+        mc = MonteCarlo.ensemble(64800, DV, DC, "bec", 0.42, 200, seed=7, batch=Be, expurgation=3)
+        mc.run_batch(0, 256)
+        torch.cuda.synchronize()
+        a.record(stream)
+        mc.run_batch(256, Be)
+        b.record(stream)
+        torch.cuda.synchronize()
+        cnt = mc.counters.cpu().numpy()
+        extras["ensemble_mc_cfg5_n64800_eps0.42_200it_X3"] = {
+            "trials_per_s": Be / (a.elapsed_time(b) * 1e-3), "batch": Be, "mean_iterations": float(cnt[3] / cnt[0]),
+            "frame_errors": int(cnt[1]), "trials": int(cnt[0])}
+        del mc
         # "optimal" modes: ML erasure decoding (parallel_simulator.py:60-129), n = 1000, eps = 0.45
         gm = TannerGraph.random_regular(1000, DV, DC, seed=1)
         wm = decoder.channel_dev("bec", 0.45, 5, 0, gm.n, 32768)
