@@ -32,6 +32,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from iib_project_ldpc_codes_amd.launch import launch_plan, spawn_ranks  # noqa: E402,F401
+
 N_BITS, DV, DC = 10000, 3, 6
 ITERS = 50
 BATCH = 65536
@@ -51,74 +53,6 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     return ap.parse_args(argv)
-
-
-def launch_plan(gpus, env, visible, rehearse=False):
-    """How this invocation runs, decided BEFORE anything initialises HIP:
-      ("single", None)  one process, one GPU (--gpus 1, no WORLD_SIZE)
-      ("rank", None)    a rank of an external launcher (torchrun: WORLD_SIZE == --gpus)
-      ("spawn", envs)   bench.py starts --gpus ranks itself, one child process per GPU, with
-                        these environments (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*)
-      ("error", msg)    refused (never a 1-GPU line for --gpus N)
-    visible = GPUs this process can see (torch.cuda.device_count(), which does not
-    initialise the runtime on this image)."""
-    if gpus < 1:
-        return "error", f"--gpus {gpus}: need at least one GPU"
-    world = env.get("WORLD_SIZE")
-    if world is not None:
-        if int(world) != gpus:
-            return "error", f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks"
-        if not rehearse and gpus > visible:
-            return "error", f"--gpus {gpus} but only {visible} GPU(s) visible"
-        return "rank", None
-    if gpus > visible and not rehearse:
-        return "error", (f"--gpus {gpus} but only {visible} GPU(s) visible to this process "
-                         f"(use --rehearse-on-one-gpu to rehearse the {gpus}-rank path on fewer devices)")
-    if gpus == 1:
-        return "single", None
-    port = env.get("MASTER_PORT") or str(_free_port())
-    envs = []
-    for r in range(gpus):
-        e = dict(env)
-        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(gpus), "LOCAL_WORLD_SIZE": str(gpus),
-                  "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port})
-        if rehearse:
-            e["LDPC_DIST_BACKEND"] = "gloo"  # ranks share a device: RCCL needs one rank per GPU
-        envs.append(e)
-    return "spawn", envs
-
-
-def _free_port():
-    import socket
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
-        sk.bind(("127.0.0.1", 0))
-        return sk.getsockname()[1]
-
-
-def spawn_ranks(envs, argv, script=None):
-    """Start one child process per rank (never exec: this process has not touched the GPU,
-    and stays the parent); rank 0's stdout (the JSON line) passes through.  Returns the
-    worst exit code; if a rank fails the others are terminated."""
-    import subprocess
-    script = script or os.path.abspath(__file__)
-    procs = [subprocess.Popen([sys.executable, "-u", script] + list(argv), env=e) for e in envs]
-    rc = 0
-    try:
-        while procs:
-            for p in list(procs):
-                c = p.poll()
-                if c is None:
-                    continue
-                procs.remove(p)
-                if c != 0:
-                    rc = rc or c
-                    for q in procs:  # a failed rank: the others would wait in a collective forever
-                        q.terminate()
-            time.sleep(0.05)
-    finally:
-        for p in procs:
-            p.kill()
-    return rc
 
 
 def host_cores():
@@ -331,7 +265,7 @@ def main():
         print(f"bench.py: {info}", file=sys.stderr, flush=True)
         return 2
     if mode == "spawn":
-        return spawn_ranks(info, sys.argv[1:])
+        return spawn_ranks(info, sys.argv[1:], script=os.path.abspath(__file__))
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

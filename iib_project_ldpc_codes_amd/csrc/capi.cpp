@@ -51,7 +51,8 @@ struct DevBuf {
 // workspace's lock, so launches on different devices / streams never serialise on g_mu.
 struct Workspace {
     std::mutex mu;
-    DevBuf trial, its, cutoff, scratch, words, llr, post, hard, errors, itsb, gchk, gvar, gatt, mlw, mlo, mlu, shape;
+    DevBuf trial, its, cutoff, scratch, words, llr, post, hard, errors, itsb, gchk, gvar, gatt, mlw, mlo, mlu, shape,
+        sctl;  // sampler search control (sample_ctl_words)
 };
 std::map<std::pair<int, void *>, Workspace> g_ws;  // (device, stream)
 
@@ -276,11 +277,6 @@ void build_lane_layout(const HostGraph &h, int T, int VPT, std::vector<int32_t> 
         lane_var[p] = v;
         for (int j = 0; j < dv; ++j) lane_slot[(size_t)p * dv + j] = pos[(size_t)v * dv + j];
     }
-#if LDPC_ABLATE_LAYOUT  // timing ablation only (wrong results): conflict-free fake positions
-    for (int p = 0; p < P; ++p)
-        for (int j = 0; j < dv; ++j) lane_slot[(size_t)p * dv + j] = (p * dv + j) % E;
-    return;
-#endif
     for (int q = 0; q < G; ++q) {
         std::vector<char> used((size_t)dv * 32, 0);  // [edge j][bank]
         for (int l = 0; l < cursor[q]; ++l)
@@ -744,7 +740,7 @@ int ldpc_bp_decode_batch_dev(const ldpc_graph *g, const float *d_llr, int B, int
     }
     if (B == 0) return LDPC_OK;
     float *scratch = nullptr;
-    const size_t sb = bp_scratch_bytes(*g, B);
+    const size_t sb = bp_scratch_bytes(*g, B, early_stop && d_post);
     if (sb) {
         std::lock_guard<std::mutex> lk(g_mu);
         Workspace &ws = workspace(stream);
@@ -788,7 +784,7 @@ int ldpc_bp_decode_batch(const int32_t *variable_to_check_list, const int32_t *c
         int32_t *di = static_cast<int32_t *>(ws.itsb.p);
         rc = 0;
         // scratch taken inside the _dev call (needs the lock released)
-        if (e == hipSuccess) e = ws.scratch.ensure(bp_scratch_bytes(*g, B));
+        if (e == hipSuccess) e = ws.scratch.ensure(bp_scratch_bytes(*g, B, early_stop && post));
         if (B > 0) {
             // no posteriors asked for: early stop may take the hard-decision path (bp_loc_kernel)
             e = launch_bp_decode(*g, dl, B, max_iters, algo, alpha, early_stop, post ? dp : nullptr, dh, di, nullptr,
@@ -855,7 +851,7 @@ int ldpc_mc_batch_dev(const ldpc_graph *g, int channel, float param, uint64_t se
     LDPC_HIP(ws.cutoff.ensure(16));
     float *scratch = nullptr;
     if (channel != LDPC_CH_BEC) {
-        const size_t sb = bp_scratch_bytes(*g, B);
+        const size_t sb = bp_scratch_bytes(*g, B, false);
         if (sb) {
             LDPC_HIP(ws.scratch.ensure(sb));
             scratch = static_cast<float *>(ws.scratch.p);
@@ -883,8 +879,11 @@ int ldpc_sample_regular_dev(int n, int dv, int dc, uint64_t seed, uint64_t first
     LDPC_REQUIRE(d_check_lookup && d_variable_lookup && G >= 0, "bad sampler arguments");
     rc = require_device();
     if (rc) return rc;
+    Workspace &ws = workspace(stream);
+    std::lock_guard<std::mutex> wl(ws.mu);
+    LDPC_HIP(ws.sctl.ensure(4 * sample_ctl_words(G)));
     LDPC_HIP(launch_sample_regular(n, dv, dc, seed, first_graph, G, d_check_lookup, d_variable_lookup, d_attempts,
-                                   1 << 20, static_cast<hipStream_t>(stream)));
+                                   1 << 20, static_cast<uint32_t *>(ws.sctl.p), static_cast<hipStream_t>(stream)));
     return LDPC_OK;
 }
 
@@ -902,9 +901,10 @@ int ldpc_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_gra
     LDPC_HIP(ws.gchk.ensure(E * G * 4));
     LDPC_HIP(ws.gvar.ensure(E * G * 4));
     LDPC_HIP(ws.gatt.ensure((size_t)G * 4 + 4));
+    LDPC_HIP(ws.sctl.ensure(4 * sample_ctl_words(G)));
     LDPC_HIP(launch_sample_regular(n, dv, dc, seed, first_graph, G, static_cast<int32_t *>(ws.gchk.p),
                                    static_cast<int32_t *>(ws.gvar.p), static_cast<int32_t *>(ws.gatt.p), 1 << 20,
-                                   nullptr));
+                                   static_cast<uint32_t *>(ws.sctl.p), nullptr));
     LDPC_HIP(hipDeviceSynchronize());
     LDPC_HIP(hipMemcpy(check_lookup, ws.gchk.p, E * G * 4, hipMemcpyDeviceToHost));
     LDPC_HIP(hipMemcpy(variable_lookup, ws.gvar.p, E * G * 4, hipMemcpyDeviceToHost));
@@ -960,8 +960,9 @@ int ldpc_sample_csr_dev(int n, int m, const int32_t *var_ptr, const int32_t *che
     const int32_t *vs, *cp, *vp;
     rc = csr_shape_upload(n, m, var_ptr, check_ptr, ws, stream, &E, &vs, &cp, &vp, &mxc, &mxv);
     if (rc) return rc;
+    LDPC_HIP(ws.sctl.ensure(4 * sample_ctl_words(G)));
     LDPC_HIP(launch_sample_csr(n, m, E, vs, cp, vp, mxc, mxv, seed, first_graph, G, d_check_var, d_var_slot, d_attempts,
-                               1 << 20, static_cast<hipStream_t>(stream)));
+                               1 << 20, static_cast<uint32_t *>(ws.sctl.p), static_cast<hipStream_t>(stream)));
     return LDPC_OK;
 }
 
@@ -980,9 +981,10 @@ int ldpc_sample_csr(int n, int m, const int32_t *var_ptr, const int32_t *check_p
     LDPC_HIP(ws.gchk.ensure((size_t)E * G * 4));
     LDPC_HIP(ws.gvar.ensure((size_t)E * G * 4));
     LDPC_HIP(ws.gatt.ensure((size_t)G * 4 + 4));
+    LDPC_HIP(ws.sctl.ensure(4 * sample_ctl_words(G)));
     LDPC_HIP(launch_sample_csr(n, m, E, vs, cp, vp, mxc, mxv, seed, first_graph, G, static_cast<int32_t *>(ws.gchk.p),
                                static_cast<int32_t *>(ws.gvar.p), static_cast<int32_t *>(ws.gatt.p), 1 << 20,
-                               nullptr));
+                               static_cast<uint32_t *>(ws.sctl.p), nullptr));
     LDPC_HIP(hipDeviceSynchronize());
     LDPC_HIP(hipMemcpy(check_var, ws.gchk.p, (size_t)E * G * 4, hipMemcpyDeviceToHost));
     LDPC_HIP(hipMemcpy(var_slot, ws.gvar.p, (size_t)E * G * 4, hipMemcpyDeviceToHost));
@@ -1014,7 +1016,9 @@ int ldpc_mc_ensemble_batch_dev(int n, int dv, int dc, int channel, float param, 
     LDPC_HIP(ws.cutoff.ensure(16));
     int32_t *chk = static_cast<int32_t *>(ws.gchk.p), *var = static_cast<int32_t *>(ws.gvar.p);
     int32_t *trial = static_cast<int32_t *>(ws.trial.p), *its = static_cast<int32_t *>(ws.its.p);
-    LDPC_HIP(launch_sample_regular(n, dv, dc, seed, first_cw, B, chk, var, nullptr, 1 << 20, s));
+    LDPC_HIP(ws.sctl.ensure(4 * sample_ctl_words(B)));
+    LDPC_HIP(launch_sample_regular(n, dv, dc, seed, first_cw, B, chk, var, nullptr, 1 << 20,
+                                   static_cast<uint32_t *>(ws.sctl.p), s));
     LDPC_HIP(launch_mc_bec_ensemble(n, dv, dc, chk, var, p, seed, first_cw, B, max_iters, trial, its, s));
     LDPC_HIP(launch_mc_reduce(trial, its, B, max_iters, expurgation, stop_frame_errors, d_counters,
                               static_cast<int32_t *>(ws.cutoff.p), s));
@@ -1113,7 +1117,9 @@ int ldpc_mc_ml_batch_dev(const ldpc_graph *g, int n, int dv, int dc, float eps, 
         LDPC_HIP(ws.gvar.ensure(E * B * 4));
         chk = static_cast<int32_t *>(ws.gchk.p);
         var = static_cast<int32_t *>(ws.gvar.p);
-        LDPC_HIP(launch_sample_regular(n, dv, dc, seed, first_cw, B, chk, var, nullptr, 1 << 20, s));
+        LDPC_HIP(ws.sctl.ensure(4 * sample_ctl_words(B)));
+        LDPC_HIP(launch_sample_regular(n, dv, dc, seed, first_cw, B, chk, var, nullptr, 1 << 20,
+                                       static_cast<uint32_t *>(ws.sctl.p), s));
     }
     // channel words of trials first_cw.. (the same Philox draws the fused BP kernels make)
     LDPC_HIP(launch_channel(LDPC_CH_BEC, p, p2, seed, first_cw, n, B, dw, s));

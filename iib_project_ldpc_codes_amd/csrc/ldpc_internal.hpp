@@ -154,9 +154,10 @@ hipError_t launch_bp_decode(const ldpc_graph &g, const float *d_llr, int B, int 
                             float alpha, int early_stop, float *d_post, uint8_t *d_hard,
                             int32_t *d_its, hipStream_t stream, float *d_scratch);
 
-// Bytes of global scratch launch_bp_decode needs for this graph/batch (0 when
-// the messages fit in LDS).
-size_t bp_scratch_bytes(const ldpc_graph &g, int B);
+// Bytes of global scratch launch_bp_decode / launch_mc_decode need for this graph/batch (0
+// when the messages fit in LDS); ep_slab: an early-stop decode that returns posteriors (the
+// local-edge kernel's per-workgroup slabs; no other mode uses them).
+size_t bp_scratch_bytes(const ldpc_graph &g, int B, bool ep_slab);
 
 hipError_t launch_channel(int channel, float p, float p2, uint64_t seed, uint64_t first_cw, int n,
                           int B, void *d_out, hipStream_t stream);
@@ -183,15 +184,18 @@ constexpr int kSeqMinE = 8192, kSeqMaxE = 393216, kSeqMaxCdeg = 192;
 // Random regular graphs on the device (law of random_code_generator.c), one
 // workgroup per graph; attempts[g] = number of permutations drawn (negative if
 // max_attempts was hit without a valid graph).
+// ctl: device scratch of sample_ctl_words(G) words for the sequential sampler's search pass
+// (nullptr: the single-pass form, one wave draws a graph's attempts in order).
 hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
                                  int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts,
-                                 int max_attempts, hipStream_t stream);
+                                 int max_attempts, uint32_t *ctl, hipStream_t stream);
+inline size_t sample_ctl_words(int G) { return 2 + 2 * (size_t)G; }
 // Irregular form: socket s of variable d_vsock[s]; check c owns slots [cptr[c], cptr[c+1]);
 // outputs check_var[g][E] and var_slot[g][E] (CSR, each variable's slots ascending).
 hipError_t launch_sample_csr(int n, int m, int E, const int32_t *d_vsock, const int32_t *d_cptr,
                              const int32_t *d_vptr, int max_cdeg, int max_vdeg, uint64_t seed, uint64_t first_graph,
                              int G, int32_t *check_var, int32_t *var_slot, int32_t *attempts, int max_attempts,
-                             hipStream_t stream);
+                             uint32_t *ctl, hipStream_t stream);
 // BEC Monte-Carlo where trial b decodes on graph b of (check_lookup, variable_lookup).
 hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,
                                   float p, uint64_t seed, uint64_t first_cw, int B, int max_iters, int32_t *trial,

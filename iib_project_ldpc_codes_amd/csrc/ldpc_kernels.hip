@@ -13,13 +13,13 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "device_common.hpp"
 #include "ldpc_internal.hpp"
 #include "ldpc_mi355x.h"
 
 namespace ldpc {
 namespace {
 
-constexpr int kWave = 64;
 #ifndef LDPC_VAR_PAIRS
 #define LDPC_VAR_PAIRS 1  // variable pairs per sched_barrier group in the LDS kernel's variable phase
 #endif
@@ -59,27 +59,6 @@ constexpr int kWave = 64;
 #ifndef LDPC_CHECK_W64
 #define LDPC_CHECK_W64 0  // check phase writes each pair edge with its own ds_write_b64
 #endif
-#ifndef LDPC_ABLATE_PHASE
-#define LDPC_ABLATE_PHASE 0    // timing ablation only: 1 = skip the check phase, 2 = skip the variable phase
-#endif
-// ---------------------------------------------------------------------------
-// Philox4x32-10 (the rocRAND philox4x32_10 stream: rocrand_init(seed,
-// subsequence = codeword, offset = 4*g) -> rocrand4 == philox_block(g, 0,
-// cw_lo, cw_hi) under key {seed_lo, seed_hi}).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                              uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-    }
-    return make_uint4(c0, c1, c2, c3);
-}
-
 __device__ __forceinline__ float u01(uint32_t x) {
     return (float)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8f;
 }
@@ -89,10 +68,6 @@ struct ChanArgs {
     float p, p2;   // see oracle_channel
     uint32_t k0, k1;
 };
-
-__device__ __forceinline__ uint32_t pick4(uint4 r, int i) {
-    return i == 0 ? r.x : (i == 1 ? r.y : (i == 2 ? r.z : r.w));
-}
 
 // Channel value of variable v of codeword cw (all-zero codeword sent).
 __device__ __forceinline__ float chan_soft(const ChanArgs &ch, uint64_t cw, int v) {
@@ -115,28 +90,6 @@ __device__ __forceinline__ uint8_t chan_bec(const ChanArgs &ch, uint64_t cw, int
 // ---------------------------------------------------------------------------
 // Block reductions (wave64)
 // ---------------------------------------------------------------------------
-// Exclusive prefix sum over the workgroup (any multiple of 64 threads <= 1024);
-// `total` gets the sum.  Contains two barriers.
-__device__ __forceinline__ int block_excl_scan(int x, int *wsum, int &total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    int incl = x;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off, kWave);
-        if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    int base = 0, tot = 0;
-    for (int w = 0; w < nw; ++w) {
-        const int v = wsum[w];
-        base += (w < wave) ? v : 0;
-        tot += v;
-    }
-    __syncthreads();
-    total = tot;
-    return base + incl - x;
-}
 
 __device__ __forceinline__ int wave_sum(int x) {
 #pragma unroll
@@ -1346,7 +1299,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             // variable phase when every check is satisfied
             int unsat = 0;
 #pragma unroll LDPC_CHECK_PAIRS_UNROLL
-            for (int q = tid; q < (LDPC_ABLATE_PHASE == 1 ? 0 : npairs); q += T) {
+            for (int q = tid; q < npairs; q += T) {
                 float2 *pp = reinterpret_cast<float2 *>(msg) + q * DC;
                 if (ET && it > 0) {
                     // the pair's 2*DC decision bytes: even bytes check 2q, odd 2q+1
@@ -1399,7 +1352,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
             // fixed-count decode: the last variable phase runs after the loop
             if (!ET && !MC && it == iters - 1) break;
             int errs = 0;
-            if constexpr (LDPC_ABLATE_PHASE != 2) {
+            {
                 if constexpr (PROD) errs = var_phase_prod(std::false_type{});
                 else errs = var_phase(std::false_type{});
             }
@@ -1603,7 +1556,6 @@ __device__ __forceinline__ uint32_t block_count(int pred, uint32_t *flag, int pa
 #endif
 
 template <int N> using int_c = std::integral_constant<int, N>;
-template <bool B> using bool_c = std::integral_constant<bool, B>;
 
 // DVN0 / DVN1: non-local edges per variable of local slot 0 / 1 (max); ABS0 / ABS1: some
 // variable of that slot has fewer (its absent edges gather the neutral value).
@@ -1932,7 +1884,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             for (int k = 0; k < KP; ++k) {
                 int q = tid + k * T;
                 asm volatile("" : "+v"(q));  // recomputed per iteration: no per-pair addresses held live
-                if (q < (LDPC_ABLATE_PHASE == 1 ? 0 : a.loc_P)) {
+                if (q < a.loc_P) {
                     if constexpr (DLO == DHI) {  // one class: rows of P pairs from word 0
                         unsat |= loc_check_pair<DLO, ALGO, false, ET && SPA>(msg, 0, a.loc_P, q, loc[2 * k],
                                                                              loc[2 * k + 1], a.alpha);
@@ -1981,7 +1933,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             if (!MC && it == iters - 1) break;  // the last variable phase only forms posteriors
             // ---- variable phase ----
             int errs = 0;
-            if constexpr (LDPC_ABLATE_PHASE != 2) {
+            {
 #pragma unroll
                 for (int k = 0; k < KP; ++k) {
                     const int d0 = var_pair(int_c<DVN0>{}, bool_c<ABS0>{}, 2 * k);
@@ -2547,554 +2499,6 @@ __global__ __launch_bounds__(kIrrT) void bp_irr_kernel(BpArgs a) {
     }
 }
 
-// ===========================================================================
-// 2c. Random regular (dv, dc) graphs: the law of random_code_generator.c:21-67
-//
-// Configuration model: a uniform permutation of the n*dv sockets, check c =
-// positions [c*dc, c*dc+dc), variable of a socket = socket / dv, and a whole-
-// graph redraw whenever a check holds a variable twice (:39-47) -- i.e. a
-// uniformly random permutation conditioned on every check being simple.  For
-// (3, 6) that condition holds with probability ~0.0074, so a graph costs ~135
-// permutations; they are drawn in parallel by one workgroup per graph with the
-// Rao-Sandelius method, which is exactly uniform:
-//   1. every socket s draws a bucket in [0, K) (K = workgroup size, the top
-//      log2 K bits of word (s>>6)&3 of Philox ctr {(s>>8)<<6 | s&63,
-//      tag|att<<2|0, g_lo, g_hi}, key = seed); a stable counting sort (bucket-major, socket order within a
-//      bucket) lays the buckets out back to back -- per-wave ranks come from
-//      log2 K ballots, offsets from a workgroup scan;
-//   2. thread t Fisher-Yates-shuffles bucket t from its end, drawing j uniform on
-//      [0, i] by Lemire's multiply-with-rejection from its own Philox stream
-//      ctr {t<<20 | block, tag|att<<2|1, g_lo, g_hi};
-//   3. every check is tested for a repeated variable; any failure redraws the
-//      whole permutation (att + 1).
-// Variable ids (socket / dv) are permuted instead of sockets: every output
-// depends on a socket only through its variable.  The permutation lives in LDS
-// (u16) when n*dv < 65536, else in the caller's check_lookup row.
-// Output: check_lookup[g][E] (variable ids, check-major) and variable_lookup
-// [g][E] (each variable's checks ascending), the reference's edge-list format.
-// oracle_sample_regular restates this bit for bit.
-// ===========================================================================
-constexpr uint32_t kSampleTag = 0x80000000u;  // never 0: channel draws use ctr[1] = 0
-
-struct BucketRng {  // sequential Philox stream of one bucket
-    uint32_t k0, k1, c0, c1, g0, g1;
-    uint32_t k = 0;
-    uint4 blk;
-    __device__ __forceinline__ uint32_t next() {
-        const uint32_t w = k & 3;
-        if (w == 0) blk = philox_block(c0 | (k >> 2), c1, g0, g1, k0, k1);
-        ++k;
-        return pick4(blk, (int)w);
-    }
-    __device__ __forceinline__ uint32_t below(uint32_t range) {  // uniform on [0, range)
-        uint64_t m = (uint64_t)next() * range;
-        uint32_t l = (uint32_t)m;
-        if (l < range) {
-            const uint32_t t = (0u - range) % range;
-            while (l < t) {
-                m = (uint64_t)next() * range;
-                l = (uint32_t)m;
-            }
-        }
-        return (uint32_t)(m >> 32);
-    }
-};
-
-// Degree structure: regular (vsock == nullptr: socket s belongs to variable s/dv,
-// check c owns slots [c*dc, c*dc+dc)) or CSR (vsock[s] = variable of socket s,
-// check c owns slots [cptr[c], cptr[c+1])).  Output, per graph: the variable of
-// every slot (check_lookup / CSR check_var) and the variable side -- regular:
-// variable_lookup[v*dv + k] = k-th check of v (ascending); CSR: var_slot[vptr[v]
-// + k] = k-th slot of v (ascending).
-struct SampleShape {
-    int n, m, E, dv, dc;
-    const int32_t *vsock, *cptr, *vptr;
-};
-
-// Variable side of a sampled graph from its check side (chk[x] = variable of
-// slot x, global): regular rows get check ids, CSR rows slot ids, each row
-// ascending (claims by atomic CAS, then a per-row insertion sort).
-__device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, int32_t *vl) {
-    const int tid = threadIdx.x, T = blockDim.x;
-    const int n = sh.n, E = sh.E, dv = sh.dv, dc = sh.dc;
-    const bool csr = sh.vsock != nullptr;
-    for (int x = tid; x < E; x += T) vl[x] = -1;
-    __threadfence_block();
-    __syncthreads();
-    for (int x = tid; x < E; x += T) {
-        const int v = chk[x];
-        int32_t *row = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
-        const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
-        const int val = csr ? x : x / dc;
-        for (int k = 0; k < deg; ++k)
-            if (atomicCAS(&row[k], -1, val) == -1) break;
-    }
-    __threadfence_block();
-    __syncthreads();
-    for (int v = tid; v < n; v += T) {
-        int32_t *r = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
-        const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
-        for (int x = 1; x < deg; ++x) {
-            const int key = r[x];
-            int y = x - 1;
-            while (y >= 0 && r[y] > key) {
-                r[y + 1] = r[y];
-                --y;
-            }
-            r[y + 1] = key;
-        }
-    }
-}
-
-// Graphs with kSeqMinE (8192) <= n*dv <= kSeqMaxE: sequential-draw sampler, one wave per
-// graph.  The same law -- a uniform socket permutation conditioned on every check
-// being simple -- drawn slot by slot, so a bad check is seen as soon as its last
-// slot is drawn and the attempt stops there (a failing (3,6) attempt at n = 64,800
-// stops after ~1/5 of the graph instead of paying a whole permutation):
-//   * slot x (in order) takes a uniform unused entry of the pool: its words --
-//     word j = word x&3 of Philox ctr {x>>2 | j<<20, tag|att<<2|3, g_lo, g_hi} --
-//     give Lemire draws on [0, R) until one lands on an unused pool index (a
-//     bitmap in LDS); 1024 words without one reject the attempt (probability
-//     < (3/4)^1000);
-//   * the pool starts as all R = E sockets; when R' = ceil(R/4) entries are left
-//     the unused ones are compacted in order into a new pool (global scratch,
-//     the variable_lookup row) with a fresh bitmap, so no draw ever sees more
-//     than 3/4 of its pool used; the last <= kSeqFinal entries are
-//     Fisher-Yates-shuffled by one lane (stream {blk, tag|1<<30|att<<2|3, g});
-//   * up to 256 consecutive slots are drawn per round, the four of block x>>2 by
-//     one lane (one Philox block per lane per word index), against the bitmap of
-//     the slots before the round; LDS atomic ORs mark the picks, and when two
-//     slots picked the same entry the round keeps only the slots below the
-//     second-lowest slot of every such group (the later slots redraw next round
-//     from the updated bitmap -- a slot's result is its first draw not used by an
-//     earlier slot, exactly the sequential process);
-//   * every check whose slots are all drawn is tested (variable ids kept in an
-//     LDS ring of the last kSeqRing slots); a repeat redraws from slot 0 (att+1).
-// ~25.6 KB of LDS per wave at n = 64,800 (the bitmap), so six graphs per CU.
-// The variable side is built with per-variable occurrence counters packed fb bits
-// per variable into the bitmap's LDS (fb = 0: global CAS, sample_emit_var_side).
-// oracle_sample_regular / oracle_sample_csr restate it bit for bit.
-constexpr int kSeqFinal = 64, kSeqRing = 512;  // ring: a round (256 slots) + the check it completes
-
-// LDS ordering between the lanes of one wave (LDS instructions of a wave execute in order):
-// a compiler barrier only -- no s_barrier, no wait for the outstanding global stores that a
-// workgroup-scope fence (__syncthreads) would add to every round
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("" ::: "memory");
-}
-
-__device__ __forceinline__ int wave_excl_scan(int v, int &total) {
-    const int lane = threadIdx.x & 63;
-    int incl = v;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const int y = __shfl_up(incl, d, kWave);
-        if (lane >= d) incl += y;
-    }
-    total = __shfl(incl, kWave - 1, kWave);
-    return incl - v;
-}
-
-template <bool CSR>  // CSR: irregular degree structure (sh.vsock / cptr / vptr)
-__global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
-                                                           uint64_t first_graph, int32_t *check_lookup,
-                                                           int32_t *variable_lookup, int32_t *attempts,
-                                                           int max_attempts, int bw, int fb, uint32_t mdv) {
-    extern __shared__ __align__(16) unsigned char smem[];
-    uint32_t *bm = reinterpret_cast<uint32_t *>(smem);  // [bw] pool bitmap, later rank counters
-    int *ring = reinterpret_cast<int *>(bm + bw);       // [kSeqRing] variable of slot x at x % kSeqRing
-    int *fin = ring + kSeqRing;                         // [kSeqFinal] last pool entries
-    const int n = sh.n, E = sh.E, m = sh.m, dv = sh.dv, dc = sh.dc;
-    constexpr bool csr = CSR;  // compile-time: the regular form has no global load in its stage-0 rounds
-    const int lane = threadIdx.x;
-    const uint64_t gid = first_graph + blockIdx.x;
-    const uint32_t g0 = (uint32_t)gid, g1 = (uint32_t)(gid >> 32);
-    int32_t *out = check_lookup + (size_t)blockIdx.x * E;
-    int32_t *vl = variable_lookup + (size_t)blockIdx.x * E;
-    // socket -> variable; regular: s / dv as a multiply-high by mdv = ceil(2^32 / dv) (exact for
-    // s < 2^24, dv < 256; mdv = 0: divide)
-    auto var_of = [&](int s) {
-        return csr ? sh.vsock[s] : (mdv ? (int)__umulhi((uint32_t)s, mdv) : s / dv);
-    };
-    auto clear_bm = [&](int words) {
-        uint4 *b4 = reinterpret_cast<uint4 *>(bm);
-        for (int w = lane; w < (words + 3) >> 2; w += kWave) b4[w] = make_uint4(0u, 0u, 0u, 0u);
-        wave_sync();
-    };
-
-    int att = 0;
-    bool ok = false;
-    while (!ok && att < max_attempts) {
-        const uint32_t c1 = kSampleTag | ((uint32_t)att << 2) | 3u;
-        int R = E, x0 = 0, cdone = 0;
-        bool bad = false;
-        // checks whose slots all lie below `upto`, from cdone on: any repeated variable?
-        auto validate = [&](int upto) -> bool {
-            int cend = cdone;
-            if constexpr (csr) {
-                for (;;) {
-                    const int c = cend + lane;
-                    const uint64_t f = __ballot(c < m && sh.cptr[c + 1] <= upto);  // a prefix of the lanes
-                    cend += __popcll(f);
-                    if (f != ~0ull) break;
-                }
-            } else {
-                cend = upto / dc;
-            }
-            bool b = false;
-            for (int cb = cdone; cb < cend; cb += kWave) {
-                const int c = cb + lane;
-                if (c < cend) {
-                    const int lo = csr ? sh.cptr[c] : c * dc, d = csr ? sh.cptr[c + 1] - lo : dc;
-                    if (d <= 8) {
-                        int v[8];
-#pragma unroll
-                        for (int a = 0; a < 8; ++a) v[a] = a < d ? ring[(lo + a) & (kSeqRing - 1)] : -1 - a;
-#pragma unroll
-                        for (int a = 0; a < 8; ++a)
-#pragma unroll
-                            for (int e = a + 1; e < 8; ++e) b |= v[a] == v[e];
-                    } else {
-                        for (int a = 0; a < d && !b; ++a) {
-                            const int va = ring[(lo + a) & (kSeqRing - 1)];
-                            for (int e = a + 1; e < d; ++e) b |= va == ring[(lo + e) & (kSeqRing - 1)];
-                        }
-                    }
-                }
-            }
-            cdone = cend;
-            return __ballot(b) == 0ull;
-        };
-
-        // the rounds of one stage (slots x0 .. xend - 1); POOL: the pool is the global row at
-        // vl + cur (stage 0: the sockets themselves -- the regular form has no global load in
-        // its rounds, so no round waits on the previous rounds' stores)
-        auto rounds = [&](auto pool_tag, int xend, int cur) {
-            constexpr bool POOL = decltype(pool_tag)::value;
-            const int32_t *pool = vl + cur;
-            const uint32_t lt = (0u - (uint32_t)R) % (uint32_t)R;  // Lemire: reject low words below this
-            while (x0 < xend) {
-                // lane L: slots 4bb .. 4bb+3 of block bb = x0/4 + L (slots below x0 are done).
-                // Word j of slot x is word x&3 of Philox {x>>2 | j<<20, c1, g}: one block per lane
-                // per word index serves its four slots.  A word is rejected by Lemire's test or
-                // when its entry is used; every slot still looking takes its next word.
-                const int base = x0 & ~3;
-                const uint32_t bb = (uint32_t)(base >> 2) + (uint32_t)lane;
-                int i[4], val[4];
-                bool act[4], need[4], dup[4];
-                bool exh = false;
-                uint4 W = philox_block(bb, c1, g0, g1, k0, k1);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int x = base + 4 * lane + q;
-                    act[q] = x >= x0 && x < xend;
-                    const uint64_t mm = (uint64_t)pick4(W, q) * (uint32_t)R;
-                    i[q] = (int)(mm >> 32);
-                    need[q] = act[q] && ((uint32_t)mm < lt || ((bm[i[q] >> 5] >> (i[q] & 31)) & 1u));
-                }
-                for (uint32_t j = 1; __ballot(need[0] || need[1] || need[2] || need[3]); ++j) {
-                    if (j >= 1024u) {  // some slot rejected 1024 words: the attempt is rejected
-                        exh = true;
-                        break;
-                    }
-                    W = philox_block(bb | (j << 20), c1, g0, g1, k0, k1);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        if (need[q]) {
-                            const uint64_t mm = (uint64_t)pick4(W, q) * (uint32_t)R;
-                            i[q] = (int)(mm >> 32);
-                            need[q] = (uint32_t)mm < lt || ((bm[i[q] >> 5] >> (i[q] & 31)) & 1u);
-                        }
-                    }
-                }
-                if (__ballot(exh)) { bad = true; return; }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    val[q] = 0;
-                    if (act[q]) val[q] = POOL ? pool[i[q]] : var_of(i[q]);
-                }
-                bool anyd = false;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t bit = 1u << (i[q] & 31);
-                    dup[q] = act[q] && (atomicOr(&bm[i[q] >> 5], bit) & bit) != 0u;
-                    anyd |= dup[q];
-                }
-                int t = min(4 * kWave, xend - base);  // kept: slots base + [x0 - base, t)
-                if (__ballot(anyd)) {
-                    // keep the slots below the second-lowest slot of every group of equal picks
-                    uint64_t dm[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) dm[q] = __ballot(dup[q]);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        while (dm[q]) {
-                            const int ip = __shfl(i[q], (int)__builtin_ctzll(dm[q]), kWave);
-                            int lo1 = 1 << 30, lo2 = 1 << 30;  // the group's two lowest slots
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                const uint64_t g = __ballot(act[r] && i[r] == ip);
-                                dm[r] &= ~g;
-                                if (g) {
-                                    const int s1 = 4 * (int)__builtin_ctzll(g) + r;
-                                    const uint64_t g2 = g & (g - 1);
-                                    const int s2 = g2 ? 4 * (int)__builtin_ctzll(g2) + r : 1 << 30;
-                                    if (s1 < lo1) { lo2 = min(lo1, s2); lo1 = s1; }
-                                    else lo2 = min(lo2, s1);
-                                }
-                            }
-                            t = min(t, lo2);
-                        }
-                    }
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)  // undo every pick of the round ...
-                        if (act[q] && !dup[q]) atomicAnd(&bm[i[q] >> 5], ~(1u << (i[q] & 31)));
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)  // ... and redo the kept ones
-                        if (act[q] && 4 * lane + q < t) atomicOr(&bm[i[q] >> 5], 1u << (i[q] & 31));
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int x = base + 4 * lane + q;
-                    if (act[q] && 4 * lane + q < t) {
-                        out[x] = val[q];
-                        ring[x & (kSeqRing - 1)] = val[q];
-                    }
-                }
-                x0 = base + t;
-                wave_sync();
-                if (!validate(x0)) { bad = true; return; }
-            }
-        };
-        // compact the unused entries of the stage's pool (R entries), in order, into dst
-        auto compact = [&](auto pool_tag, int cur, auto *dst) {
-            constexpr bool POOL = decltype(pool_tag)::value;
-            const int32_t *pool = vl + cur;
-            const int words = (R + 31) >> 5;
-            int base = 0;
-            for (int w0 = 0; w0 < words; w0 += kWave) {
-                const int w = w0 + lane;
-                uint32_t un = 0u;
-                if (w < words) {
-                    un = ~bm[w];
-                    const int valid = R - w * 32;
-                    if (valid < 32) un &= (1u << valid) - 1u;
-                }
-                int tot = 0;
-                int o = base + wave_excl_scan(__popc(un), tot);
-                while (un) {
-                    const int b = __ffs(un) - 1;
-                    un &= un - 1u;
-                    const int idx = w * 32 + b;
-                    dst[o++] = POOL ? pool[idx] : var_of(idx);
-                }
-                base += tot;
-            }
-        };
-
-        clear_bm((R + 31) >> 5);
-        int cur = -1;  // offset of the current pool in vl (-1: stage 0, the sockets)
-        while (R > kSeqFinal && !bad) {
-            const int Rn = (R + 3) >> 2, xend = E - Rn;
-            if (cur < 0) rounds(bool_c<false>{}, xend, 0);
-            else rounds(bool_c<true>{}, xend, cur);
-            if (bad) break;
-            if (Rn <= kSeqFinal) {  // the last entries go to LDS
-                if (cur < 0) compact(bool_c<false>{}, 0, fin);
-                else compact(bool_c<true>{}, cur, fin);
-            } else {  // the next pool: vl[0 ..) and vl[E/2 ..) alternately (R' <= E/4 + 1)
-                const int nx = cur == 0 ? E / 2 : 0;
-                if (cur < 0) compact(bool_c<false>{}, 0, vl + nx);
-                else compact(bool_c<true>{}, cur, vl + nx);
-                cur = nx;
-            }
-            __threadfence_block();
-            __syncthreads();
-            R = Rn;
-            clear_bm((R + 31) >> 5);
-        }
-        if (!bad) {
-            // last R <= kSeqFinal entries (in fin): Fisher-Yates by lane 0, then the last slots
-            if (R == E && lane < E) fin[lane] = var_of(lane);  // tiny graphs: no compaction ran
-            wave_sync();
-            if (lane == 0) {
-                BucketRng rng{k0, k1, 0u, c1 | (1u << 30), g0, g1};
-                for (int a = R - 1; a >= 1; --a) {
-                    const int j = (int)rng.below((uint32_t)a + 1u);
-                    const int tmp = fin[a];
-                    fin[a] = fin[j];
-                    fin[j] = tmp;
-                }
-            }
-            wave_sync();
-            if (lane < R) {
-                const int x = x0 + lane;
-                out[x] = fin[lane];
-                ring[x & (kSeqRing - 1)] = fin[lane];
-            }
-            wave_sync();
-            bad = !validate(E);
-        }
-        ok = !bad;
-        ++att;
-    }
-    if (attempts && lane == 0) attempts[blockIdx.x] = ok ? att : -att;
-    if (!ok)  // max_attempts without a simple graph: the identity configuration (in-range ids)
-        for (int x = lane; x < E; x += kWave) out[x] = var_of(x);
-    __threadfence_block();
-    __syncthreads();
-    if (fb == 0) {
-        sample_emit_var_side(sh, out, vl);
-        return;
-    }
-    // variable side: occurrence rank of each slot's variable from fb-bit LDS counters
-    // (slot order, so rows come out nearly ascending), then a per-row insertion sort
-    clear_bm(bw);
-    const uint32_t fmask = (1u << fb) - 1u;
-    for (int xb = 0; xb < E; xb += kWave) {
-        const int x = xb + lane;
-        if (x < E) {
-            const int v = out[x];
-            const uint32_t pos = (uint32_t)v * (uint32_t)fb;
-            const uint32_t old = atomicAdd(&bm[pos >> 5], 1u << (pos & 31));
-            const int rank = (int)((old >> (pos & 31)) & fmask);
-            if (csr) vl[sh.vptr[v] + rank] = x;
-            else vl[(size_t)v * dv + rank] = x / dc;
-        }
-    }
-    __threadfence_block();
-    __syncthreads();
-    for (int v = lane; v < n; v += kWave) {
-        int32_t *r = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
-        const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
-        for (int x = 1; x < deg; ++x) {
-            const int key = r[x];
-            int y = x - 1;
-            while (y >= 0 && r[y] > key) {
-                r[y + 1] = r[y];
-                --y;
-            }
-            r[y + 1] = key;
-        }
-    }
-}
-
-template <int T, typename Idx, bool LDSBUF>
-__global__ __launch_bounds__(T) void sample_regular_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
-                                                           uint64_t first_graph, int32_t *check_lookup,
-                                                           int32_t *variable_lookup, int32_t *attempts,
-                                                           int max_attempts) {
-    constexpr int NW = T / kWave;
-    constexpr int LOGK = T == 256 ? 8 : (T == 512 ? 9 : 10);
-    extern __shared__ __align__(16) unsigned char smem[];
-    int *cnt = reinterpret_cast<int *>(smem);  // [T buckets][NW waves]
-    int *wsum = cnt + T * NW;                  // [16]
-    const int E = sh.E, m = sh.m, dv = sh.dv, dc = sh.dc;
-    const bool csr = sh.vsock != nullptr;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t gid = first_graph + blockIdx.x;
-    const uint32_t g0 = (uint32_t)gid, g1 = (uint32_t)(gid >> 32);
-    int32_t *chk = check_lookup + (size_t)blockIdx.x * E;
-    Idx *buf = LDSBUF ? reinterpret_cast<Idx *>(wsum + 16) : reinterpret_cast<Idx *>(chk);
-    const int chunk = ((E + NW - 1) / NW + 255) / 256 * 256;
-    const int s_lo = min(E, wave * chunk), s_hi = min(E, s_lo + chunk);
-    const uint64_t lt_mask = (1ull << lane) - 1;
-
-    // bucket of socket s = base + lane (base a multiple of 64) from word (s>>6)&3 of
-    // the Philox block {(s>>8)<<6 | lane, c1, g}: one block per lane per 256 sockets;
-    // peers = the lanes of this 64-socket group in the same bucket
-    auto group = [&](int base, const uint4 &r, uint32_t &bk, uint64_t &peers) {
-        const int s = base + lane;
-        const bool valid = s < s_hi;
-        bk = valid ? pick4(r, (base >> 6) & 3) >> (32 - LOGK) : 0u;
-        peers = __ballot(valid);
-#pragma unroll
-        for (int bit = 0; bit < LOGK; ++bit) {
-            const bool on = (bk >> bit) & 1u;
-            const uint64_t bal = __ballot(valid && on);
-            peers &= on ? bal : ~bal;
-        }
-        return valid;
-    };
-
-    int att = 0;
-    bool ok = false;
-    while (!ok && att < max_attempts) {
-        const uint32_t c1 = kSampleTag | ((uint32_t)att << 2);
-        for (int i = tid; i < T * NW; i += T) cnt[i] = 0;
-        __syncthreads();
-        // 1a. bucket sizes per (bucket, wave)
-        for (int b256 = s_lo; b256 < s_hi; b256 += 256) {
-            const uint4 r = philox_block((uint32_t)(((b256 >> 8) << 6) | lane), c1, g0, g1, k0, k1);
-            for (int base = b256; base < min(s_hi, b256 + 256); base += 64) {
-                uint32_t bk;
-                uint64_t peers;
-                if (group(base, r, bk, peers) && (peers & lt_mask) == 0) cnt[bk * NW + wave] += __popcll(peers);
-            }
-        }
-        __syncthreads();
-        // 1b. offsets: bucket-major, wave-minor (= socket order inside a bucket)
-        int size = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) size += cnt[tid * NW + w];
-        int total = 0;
-        const int start = block_excl_scan(size, wsum, total);
-        {
-            int run = start;
-#pragma unroll
-            for (int w = 0; w < NW; ++w) {
-                const int c = cnt[tid * NW + w];
-                cnt[tid * NW + w] = run;
-                run += c;
-            }
-        }
-        __syncthreads();
-        // 1c. stable scatter of the variable ids
-        for (int b256 = s_lo; b256 < s_hi; b256 += 256) {
-            const uint4 r = philox_block((uint32_t)(((b256 >> 8) << 6) | lane), c1, g0, g1, k0, k1);
-            for (int base = b256; base < min(s_hi, b256 + 256); base += 64) {
-                uint32_t bk;
-                uint64_t peers;
-                if (group(base, r, bk, peers)) {
-                    const int s = base + lane;
-                    const int dst = cnt[bk * NW + wave] + __popcll(peers & lt_mask);
-                    buf[dst] = (Idx)(csr ? sh.vsock[s] : s / dv);
-                    if ((peers & lt_mask) == 0) cnt[bk * NW + wave] += __popcll(peers);
-                }
-            }
-        }
-        __syncthreads();
-        // 2. Fisher-Yates inside bucket `tid`
-        {
-            BucketRng rng{k0, k1, (uint32_t)tid << 20, c1 | 1u, g0, g1};
-            Idx *bb = buf + start;
-            for (int i = size - 1; i >= 1; --i) {
-                const int j = (int)rng.below((uint32_t)i + 1u);
-                const Idx t = bb[i];
-                bb[i] = bb[j];
-                bb[j] = t;
-            }
-        }
-        __syncthreads();
-        // 3. every check simple?
-        int bad = 0;
-        for (int c = tid; c < m; c += T) {
-            const int lo = csr ? sh.cptr[c] : c * dc, d = csr ? sh.cptr[c + 1] - lo : dc;
-            const Idx *r = buf + lo;
-            for (int x = 0; x < d && !bad; ++x)
-                for (int y = x + 1; y < d; ++y) bad |= (r[x] == r[y]);
-        }
-        ok = !__syncthreads_or(bad);
-        ++att;
-    }
-    if (attempts && tid == 0) attempts[blockIdx.x] = ok ? att : -att;
-    // check_lookup (variable ids per slot); variable_lookup rows claimed by CAS, then sorted
-    int32_t *vl = variable_lookup + (size_t)blockIdx.x * E;
-    if (LDSBUF)
-        for (int x = tid; x < E; x += T) chk[x] = buf[x];
-    sample_emit_var_side(sh, chk, vl);
-}
 
 // ===========================================================================
 // 3. Stand-alone channel (rocRAND philox4x32_10 device API)
@@ -3481,12 +2885,6 @@ __global__ __launch_bounds__(1024) void ml_kernel(const int32_t *__restrict__ cp
 // ===========================================================================
 constexpr size_t kLdsMax = 160 * 1024;
 
-template <typename K>
-hipError_t allow_lds(K kernel, size_t bytes) {
-    if (bytes <= 64 * 1024) return hipSuccess;
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-}
 
 ChanArgs make_chan(int kind, float p, float p2, uint64_t seed) {
     ChanArgs c;
@@ -3626,14 +3024,13 @@ enum class BpPath { Loc, Lds36, Irr, Generic8, Generic16, Generic32, GenericG8, 
 // x (threads, check pairs per thread)
 // Early stop with posteriors on bp_loc_kernel: persistent workgroups (two per CU, the most
 // any bp_loc_kernel shape keeps resident), each with a VP x T float2 slab in scratch.
+// The CU count is queried for the current device on every call (no shared cache: devices
+// launch from their own host threads, and the slab size and the grid must agree per device).
 int loc_ep_grid() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-    }
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
     return 2 * cus;
 }
 size_t loc_ep_slab_floats(const ldpc_graph &g) {
@@ -3682,9 +3079,10 @@ BpPath choose_path(const ldpc_graph &g, int iters, bool et, bool mc, int algo = 
     // is faster (its variable sums need no reordering); with the two-workgroup 512-thread
     // shape the local-edge kernel wins (bench code: 2.00 vs 1.74 M cw/s); the local-edge
     // kernel for everything else it covers
-    // (Monte-Carlo with or without early stop; early-stop decodes that return posteriors stay
-    // on the other kernels, hard-decision-only ones run here; min-sum early stop: one check
-    // class)
+    // (Monte-Carlo with or without early stop; early-stop decodes with hard decisions only;
+    // early-stop decodes that return posteriors when the message LDS can stage n posteriors +
+    // n decision bytes (ep_ok: the persistent grid with per-workgroup slabs); min-sum early
+    // stop: one check class)
     const bool lds36_ms = LDPC_LDS36_MINSUM && algo == 1 && g.lane_var && g.dv == 3 && g.dc == 6 && g.loc_T != 512;
     const bool one_cls = loc_variant_of(g) == kLocReg36;  // the one-class (3,6) instantiation
     // early stop with posteriors stages n posteriors + n decision bytes in the message LDS
@@ -3913,7 +3311,7 @@ hipError_t launch_bec_decode(const ldpc_graph &g, uint8_t *d_words, int B, int m
     return run_bec<false>(g, a, B, stream);
 }
 
-size_t bp_scratch_bytes(const ldpc_graph &g, int B) {
+size_t bp_scratch_bytes(const ldpc_graph &g, int B, bool ep_slab) {
     const int grid = B < LDPC_GMEM_GRID ? B : LDPC_GMEM_GRID;
     // the irregular kernel's slab (if any) and, for iteration counts that push
     // it off LDS, the generic kernel's: enough for whichever path runs
@@ -3921,7 +3319,7 @@ size_t bp_scratch_bytes(const ldpc_graph &g, int B) {
     const size_t per = ((size_t)g.E * 5 + (size_t)g.n * 4 + 15) & ~(size_t)15;
     const size_t gen = generic_lds_bytes(g, 0, true) + 4096 <= kLdsMax ? 0 : per * (size_t)grid;
     // bp_loc_kernel early stop with posteriors: per-workgroup slabs + the codeword counter
-    const size_t loc = g.loc_KP ? loc_ep_slab_floats(g) * 4 + 64 : 0;
+    const size_t loc = ep_slab && g.loc_KP ? loc_ep_slab_floats(g) * 4 + 64 : 0;
     return std::max(std::max(irr, gen), loc);
 }
 
@@ -3996,67 +3394,6 @@ hipError_t launch_mc_decode(const ldpc_graph &g, int channel, float p, float p2,
     a.its = trial_its;
     a.scratch = d_scratch;
     return dispatch_bp_algo<true>(g, a, algo, early_stop, stream);
-}
-
-static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vdeg, uint64_t seed,
-                                uint64_t first_graph, int G, int32_t *check_lookup, int32_t *variable_lookup,
-                                int32_t *attempts, int max_attempts, hipStream_t stream) {
-    if (G <= 0) return hipSuccess;
-    const int E = sh.E;
-    const int K = sample_buckets(E);
-    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const size_t ctl = (size_t)4 * (K * (K / kWave) + 16);
-    const bool u16 = sh.n <= 65536;
-#define LDPC_SAMPLE(TT, IDX, LDSB)                                                                             \
-    do {                                                                                                       \
-        auto k = sample_regular_kernel<TT, IDX, LDSB>;                                                         \
-        const size_t lds = ctl + (LDSB ? (size_t)2 * E : 0);                                                   \
-        hipError_t e = allow_lds(k, lds);                                                                      \
-        if (e != hipSuccess) return e;                                                                         \
-        hipLaunchKernelGGL(k, dim3(G), dim3(TT), lds, stream, sh, k0, k1, first_graph, check_lookup,           \
-                           variable_lookup, attempts, max_attempts);                                           \
-        return hipGetLastError();                                                                              \
-    } while (0)
-    // LDPC_SEQ_MIN_E: timing experiments only (the oracle follows kSeqMinE)
-    static const int seq_min = getenv("LDPC_SEQ_MIN_E") ? atoi(getenv("LDPC_SEQ_MIN_E")) : kSeqMinE;
-    const bool seq = E >= seq_min && E <= kSeqMaxE && max_cdeg <= kSeqMaxCdeg;
-    if (K == 256 && u16 && !seq) LDPC_SAMPLE(256, uint16_t, true);
-    if (K == 512 && u16 && !seq) LDPC_SAMPLE(512, uint16_t, true);
-    if (seq) {
-        // bitmap words (a multiple of 4: cleared with 16-byte stores); rank counters of
-        // fb bits per variable share them when they fit
-        int bw = ((E + 31) / 32 + 3) & ~3;
-        const int fb = max_vdeg <= 3 ? 2 : (max_vdeg <= 15 ? 4 : (max_vdeg <= 255 ? 8 : 0));
-        const int fbu = fb && (long)sh.n * fb <= (long)bw * 32 ? fb : 0;
-        const size_t lds = (size_t)4 * (bw + kSeqRing + kSeqFinal);
-        auto kern = sh.vsock ? sample_seq_kernel<true> : sample_seq_kernel<false>;
-        hipError_t e = allow_lds(kern, lds);
-        if (e != hipSuccess) return e;
-        const uint32_t mdv =
-            sh.vsock == nullptr && sh.dv > 1 && sh.dv < 256 ? (uint32_t)((0x100000000ull + sh.dv - 1) / sh.dv) : 0u;
-        hipLaunchKernelGGL(kern, dim3(G), dim3(kWave), lds, stream, sh, k0, k1, first_graph,
-                           check_lookup, variable_lookup, attempts, max_attempts, bw, fbu, mdv);
-        return hipGetLastError();
-    }
-    LDPC_SAMPLE(1024, int32_t, false);
-#undef LDPC_SAMPLE
-}
-
-hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
-                                 int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts,
-                                 int max_attempts, hipStream_t stream) {
-    const SampleShape sh{n, n * dv / dc, n * dv, dv, dc, nullptr, nullptr, nullptr};
-    return launch_sample(sh, dc, dv, seed, first_graph, G, check_lookup, variable_lookup, attempts, max_attempts,
-                         stream);
-}
-
-hipError_t launch_sample_csr(int n, int m, int E, const int32_t *d_vsock, const int32_t *d_cptr,
-                             const int32_t *d_vptr, int max_cdeg, int max_vdeg, uint64_t seed, uint64_t first_graph,
-                             int G, int32_t *check_var, int32_t *var_slot, int32_t *attempts, int max_attempts,
-                             hipStream_t stream) {
-    const SampleShape sh{n, m, E, 0, 0, d_vsock, d_cptr, d_vptr};
-    return launch_sample(sh, max_cdeg, max_vdeg, seed, first_graph, G, check_var, var_slot, attempts, max_attempts,
-                         stream);
 }
 
 hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,

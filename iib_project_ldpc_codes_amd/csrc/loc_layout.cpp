@@ -444,11 +444,6 @@ bool build_loc_layout(int n, int m, const std::vector<int32_t> &cptr, const std:
                             ++u;
                         }
                     for (; u < DVN; ++u) pk[u] |= (uint32_t)(dummy + (t & 63)) << (16 * h);
-#if LDPC_ABLATE_LOC_LAYOUT  // timing ablation only (wrong results): conflict-free gather words
-                    for (int uu = 0; uu < DVN; ++uu)
-                        pk[uu] = (pk[uu] & ~(0xffffu << (16 * h))) |
-                                 (uint32_t)((((vi * DVN + uu) * 2 + h) * 64 + (t & 63)) % L.words) << (16 * h);
-#endif
                     info |= (uint32_t)jl << (8 + 2 * h);
                     if (v >= 0 && jl < 4) info |= 1u << (16 + 4 * h + jl);  // one-hot copy (min-sum masks)
                 }

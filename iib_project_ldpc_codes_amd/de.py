@@ -121,3 +121,34 @@ def sigma_to_ebn0_db(sigma, rate):
 
 def regular(dv, dc):
     return Ensemble({dv: 1.0}, {dc: 1.0})
+
+
+# ------------------------------------------------- finite-length scaling (BEC)
+
+
+def scaling_threshold_y(eps_star, dv, dc, tol=1e-6):
+    """Fixed point y of y = 1 - (1 - eps* y^(dv-1))^(dc-1) at the threshold, iterated from 1
+    (finite_length_scaling_calculation.py:9-16)."""
+    prev, y = 0.0, 1.0
+    while abs(y - prev) > tol:
+        prev = y
+        y = 1.0 - (1.0 - eps_star * y ** (dv - 1)) ** (dc - 1)
+    return y
+
+
+def scaling_alpha(eps_star, dv, dc):
+    """Scaling parameter alpha of the (dv, dc) ensemble on the BEC
+    (finite_length_scaling_calculation.py:18-21)."""
+    y = scaling_threshold_y(eps_star, dv, dc)
+    x = eps_star * y ** (dv - 1)
+    return eps_star * np.sqrt(((dv - 1) / dv) * (1.0 / x - 1.0 / y))
+
+
+def scaling_fer(n, eps, eps_star, alpha, beta=0.616949):
+    """Waterfall block-error probability of the length-n ensemble under BP on BEC(eps):
+    Q(sqrt(n) (eps* - beta n^(-2/3) - eps) / alpha) -- the law of
+    finite_length_scaling_calculation.py:37-43 with the shift term of its :40 and the
+    (3,6) shift beta = 0.616949 of tools/density_evolution.py:3-6."""
+    from scipy.stats import norm
+    z = np.sqrt(n) * (eps_star - beta * n ** (-2.0 / 3.0) - np.asarray(eps, dtype=np.float64))
+    return norm.cdf(-z / alpha)

@@ -1,19 +1,24 @@
-"""Time ldpc_sample_regular_dev per library build (sampler ablations).
-usage: python scripts/diag/sampler_time.py lib1.so lib2.so ..."""
+"""Time ldpc_sample_regular_dev per library build (sampler variants).
+usage: python scripts/diag/sampler_time.py [--sizes n:G,n:G,...] lib1.so lib2.so ..."""
 import ctypes as ct, os, sys
 sys.path.insert(0, os.getcwd())
 import torch
-import numpy as np
-for p in sys.argv[1:]:
+
+sizes = [(1000, 16384), (10000, 4096), (64800, 512), (64800, 16384)]
+args = sys.argv[1:]
+if args and args[0] == "--sizes":
+    sizes = [tuple(int(v) for v in s.split(":")) for s in args[1].split(",")]
+    args = args[2:]
+for p in args:
     L = ct.CDLL(os.path.abspath(p), mode=os.RTLD_LOCAL)
     L.ldpc_sample_regular_dev.argtypes = [ct.c_int] * 3 + [ct.c_uint64] * 2 + [ct.c_int] + [ct.c_void_p] * 4
-    for n, G in ((1000, 16384), (10000, 4096), (64800, 512)):
+    for n, G in sizes:
         chk = torch.empty((G, n * 3), dtype=torch.int32, device="cuda")
         var = torch.empty_like(chk)
         att = torch.empty(G, dtype=torch.int32, device="cuda")
         s = torch.cuda.current_stream()
         ts = []
-        for r in range(3):
+        for r in range(2):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(s)
             assert L.ldpc_sample_regular_dev(n, 3, 6, 5, r * G, G, chk.data_ptr(), var.data_ptr(), att.data_ptr(),
@@ -24,3 +29,4 @@ for p in sys.argv[1:]:
         A = att.float().abs().mean().item()
         print(f"{os.path.basename(p):28s} n={n:6d} G={G:6d} {min(ts):9.2f} ms  {G / min(ts) * 1e3:10.0f} graphs/s  "
               f"mean attempts {A:6.1f}  us/attempt/graph {min(ts) * 1e3 / (G * A):8.3f}", flush=True)
+        del chk, var, att

@@ -5,12 +5,14 @@
         BI-AWGN, SPA, 100 it
   ens:  BASELINE configs[4] -- expurgated (3,6) ensemble (a fresh device-sampled graph per
         trial, parallel_simulator_expurgated.py), n=64800, BEC, 200 it, expurgation X=3
-One process per GPU (torchrun); trials shard by index, counters all-reduced per round.
-Each point stops at --stop-errors frame errors (200, parallel_simulator.py:198), --trials,
-or --seconds.
+One process per GPU: `--gpus N` starts the N ranks itself (decided before any HIP call, refused
+when fewer than N GPUs are visible -- iib_project_ldpc_codes_amd/launch.py, the same plan as
+bench.py), or runs as a rank of an external torchrun; trials shard by index, counters are
+all-reduced per round.  Each point stops at --stop-errors frame errors (200,
+parallel_simulator.py:198), --trials, or --seconds.
 
   python scripts/fer_sweep.py cfg3 [--trials 1000000] [--seconds 60]
-  torchrun --nproc-per-node 8 scripts/fer_sweep.py cfg4 --seconds 300
+  python scripts/fer_sweep.py cfg4 --gpus 8 --seconds 300
 """
 import argparse
 import json
@@ -24,11 +26,12 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from iib_project_ldpc_codes_amd import de, ensembles, snapshot  # noqa: E402
+from iib_project_ldpc_codes_amd.launch import launch_plan, spawn_ranks  # noqa: E402
 from iib_project_ldpc_codes_amd.graph import TannerGraph  # noqa: E402
 from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo  # noqa: E402
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("config", choices=["cfg3", "cfg4", "ens"])
     ap.add_argument("--trials", type=int, default=1_000_000)
@@ -41,12 +44,31 @@ def main():
     ap.add_argument("--stop-errors", type=int, default=200)
     ap.add_argument("--deg2", default="path", help="cfg4 degree-2 placement (ensembles.sample_irregular)")
     ap.add_argument("--expurgation", type=int, default=3, help="ens: X (parallel_simulator_expurgated.py argv[9])")
-    args = ap.parse_args()
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one process per GPU (default: torchrun's WORLD_SIZE, else 1); "
+                         "without WORLD_SIZE the sweep starts them itself")
+    ap.add_argument("--rehearse-on-one-gpu", action="store_true",
+                    help="allow more ranks than visible GPUs (shared devices, gloo): a rehearsal only")
+    args = ap.parse_args(argv)
+    if args.gpus is None:
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
+    return args
+
+
+def main(argv=None):
+    args = parse(argv)
+    # decided before anything initialises HIP (device_count does not, on this image)
+    mode, info = launch_plan(args.gpus, os.environ, torch.cuda.device_count(), args.rehearse_on_one_gpu)
+    if mode == "error":
+        print(f"fer_sweep: {info}", file=sys.stderr)
+        return 2
+    if mode == "spawn":
+        return spawn_ranks(info, sys.argv[1:] if argv is None else list(argv), script=os.path.abspath(__file__))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("LDPC_DIST_BACKEND", "nccl"))
     rank = dist.get_rank() if world > 1 else 0
     if args.config == "cfg3":
         g = TannerGraph.random_regular(10000, 3, 6, seed=1, distinct_columns=True)
@@ -94,7 +116,8 @@ def main():
             print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
