@@ -185,9 +185,9 @@ def onchip_rooflines(cw_iters_per_s, kernel):
     execution counts, cross-checked with and completed by the PMC counters of one launch):
       valu: issue cycles per codeword-iteration (packed f32 4, plain 2, transcendental 8 per
             wave64 instruction, MI355X_MICROARCH.md) over 1024 SIMDs x 2.4 GHz;
-      lds:  LDS cycles per codeword-iteration (conflict-free per-instruction costs of the
-            MI355X_MICROARCH.md LDS table; the measured bank-conflict cycles are reported
-            beside it as waste) over 256 CUs x 2.4 GHz.
+      lds:  LDS cycles per codeword-iteration -- the conflict-free per-instruction costs of the
+            MI355X_MICROARCH.md LDS table PLUS the measured SQ_LDS_BANK_CONFLICT cycles (the pipe
+            is busy for both) -- over 256 CUs x 2.4 GHz; the conflict-free fraction beside it.
     achieved = cycles x the live codeword-iteration rate of the kernel.  Returns (valu, lds), or
     (None, None) when the committed model is of another kernel than the one that ran."""
     if not os.path.exists(ISSUE_PROFILE):
@@ -218,9 +218,12 @@ def onchip_rooflines(cw_iters_per_s, kernel):
         valu["pmc_profile"] = os.path.relpath(prof_pmc, ROOT)
     elif pmc:
         valu["pmc_valu_active_frac"] = None
-    lds = {"bound": "lds", "achieved": l_cyc * cw_iters_per_s / 1e9, "peak": CUS * CLOCK_HZ / 1e9,
-           "unit": "G LDS-cycles/s", "frac": l_cyc * cw_iters_per_s / (CUS * CLOCK_HZ),
-           "lds_cycles_per_codeword_iteration": l_cyc,
+    conf = d["lds_bank_conflict_cycles_per_codeword_iteration"]
+    lds = {"bound": "lds", "achieved": (l_cyc + conf) * cw_iters_per_s / 1e9, "peak": CUS * CLOCK_HZ / 1e9,
+           "unit": "G LDS-cycles/s", "frac": (l_cyc + conf) * cw_iters_per_s / (CUS * CLOCK_HZ),
+           "conflict_free_frac": l_cyc * cw_iters_per_s / (CUS * CLOCK_HZ),
+           "lds_cycles_per_codeword_iteration": l_cyc + conf,
+           "conflict_free_lds_cycles_per_codeword_iteration": l_cyc,
            "lds_instr_per_codeword_iteration": d["lds_instr_per_codeword_iteration"],
            "bank_conflict_cycles_per_codeword_iteration": d["lds_bank_conflict_cycles_per_codeword_iteration"],
            "cycles_per_wave_instr": d["cycles"]["lds"], "profile": rel, "profile_git": d.get("git")}

@@ -887,6 +887,19 @@ int ldpc_sample_regular_dev(int n, int dv, int dc, uint64_t seed, uint64_t first
     return LDPC_OK;
 }
 
+int ldpc_debug_seq_stats(uint64_t *out, int reset) {
+    LDPC_REQUIRE(out, "null output");
+    int rc = require_device();
+    if (rc) return rc;
+    const hipError_t e = seq_stats(out, reset);
+    if (e == hipErrorNotSupported) {
+        set_error("sampler statistics need a -DLDPC_SEQ_STATS=1 build");
+        return LDPC_EUNSUP;
+    }
+    LDPC_HIP(e);
+    return LDPC_OK;
+}
+
 int ldpc_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G, int32_t *check_lookup,
                         int32_t *variable_lookup, int32_t *attempts) {
     int rc = check_regular_shape(n, dv, dc);

@@ -183,6 +183,47 @@ __device__ __forceinline__ void seq_clear_bm(uint32_t *bm, int words) {
 
 constexpr uint32_t kSeqNone = 0xFFFFFFFFu;  // search: no simple attempt found (yet)
 
+// Diagnostics build only (-DLDPC_SEQ_STATS=1, scripts/build_variants.sh): the search pass
+// accumulates per-launch counts and s_memtime cycles by phase into g_seq_stats
+// (ldpc_debug_seq_stats); the product build compiles every SEQ_STAT to nothing.
+#ifndef LDPC_SEQ_STATS
+#define LDPC_SEQ_STATS 0
+#endif
+enum SeqStat {
+    kStAttempts, kStAborted, kStRounds, kStKept, kStLaneIters, kStSpreadIters, kStCollRounds, kStProbes,
+    kStCycAttempt, kStCycDraw, kStCycRetry, kStCycMark, kStCycRingVal, kStCycCompact, kStCycClaim, kStValFail,
+    kStCount
+};
+__device__ unsigned long long g_seq_stats[kStCount];
+struct SeqStats {
+    unsigned long long v[kStCount];
+    uint64_t t;  // last time stamp
+    __device__ void zero() {
+        for (int i = 0; i < kStCount; ++i) v[i] = 0;
+        t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ void lap(int i) {  // cycles since the last stamp into v[i]
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        v[i] += now - t;
+        t = now;
+    }
+    __device__ void flush() {
+        if ((threadIdx.x & 63) == 0)
+            for (int i = 0; i < kStCount; ++i)
+                if (v[i]) atomicAdd(&g_seq_stats[i], v[i]);
+    }
+};
+#if LDPC_SEQ_STATS
+#define SEQ_STAT(st, expr) \
+    do {                   \
+        if (st) { expr; }  \
+    } while (0)
+#else
+#define SEQ_STAT(st, expr) \
+    do {                   \
+    } while (0)
+#endif
+
 // Attempt `att` of the sequential draw (one wave).  EMIT: every slot's variable also goes to
 // out[x] (the emit pass); otherwise only the verdict matters (the search pass).  pools: >= E
 // ints of global scratch (the stage pools, two halves used alternately).  best != nullptr
@@ -190,7 +231,8 @@ constexpr uint32_t kSeqNone = 0xFFFFFFFFu;  // search: no simple attempt found (
 // wave) is below att -- it can no longer be the graph's first simple attempt.
 // Returns true when the attempt drew a simple graph.
 template <bool CSR, bool EMIT>
-__device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *pools, const uint32_t *best) {
+__device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *pools, const uint32_t *best,
+                            SeqStats *st = nullptr) {
     const int lane = threadIdx.x & 63;
     const int E = c.sh.E, m = c.sh.m, dc = c.sh.dc;
     const uint32_t k0 = c.k0, k1 = c.k1, g0 = c.g0, g1 = c.g1;
@@ -199,6 +241,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
     int *const tl = c.tl;
     const uint32_t c1 = kSampleTag | ((uint32_t)att << 2) | 3u;
     int R = E, x0 = 0, cdone = 0, nround = 0;
+    uint32_t bseen = kSeqNone;  // search: *best as last loaded
     bool bad = false;
     // checks whose slots all lie below `upto`, from cdone on: any repeated variable?
     auto validate = [&](int upto) -> bool {
@@ -266,8 +309,13 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
         };
         while (x0 < xend) {
             if (best && (++nround & 15) == 0) {  // search: a lower simple attempt makes this one moot
-                const uint32_t bnow = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (__builtin_amdgcn_readfirstlane(bnow) < (uint32_t)att) { bad = true; return; }
+                // (the value loaded 16 rounds ago: the load's latency never stalls a round)
+                if (__builtin_amdgcn_readfirstlane(bseen) < (uint32_t)att) {
+                    SEQ_STAT(st, st->v[kStAborted]++);
+                    bad = true;
+                    return;
+                }
+                bseen = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             // lane L: slots 4bb .. 4bb+3 of block bb = x0/4 + L (slots below x0 are done).
             // Word j of slot x is word x&3 of Philox {x>>2 | j<<20, c1, g}.  A slot takes its
@@ -276,6 +324,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             // the next block of its own four slots; once at most 32 do, the wave spreads them --
             // L = 2..32 lanes per slot, each trying one of the slot's next L words, the lowest
             // passing word wins (a slot's words are tried in order, so the result is the same).
+            SEQ_STAT(st, st->v[kStRounds]++; st->lap(kStCycRingVal));
             const int base = x0 & ~3;
             const uint32_t bb = (uint32_t)(base >> 2) + (uint32_t)lane;
             int i[4];
@@ -290,6 +339,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                     need[q] = act[q] && i[q] < 0;
                 }
             }
+            SEQ_STAT(st, st->lap(kStCycDraw));
             uint32_t j0 = 1;  // next word index of every slot still looking
             for (;;) {
                 uint64_t mq[4];
@@ -302,6 +352,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 if (C == 0) break;
                 if (j0 >= 1024u) { bad = true; return; }  // a slot rejected 1024 words: reject the attempt
                 if (C > 32) {  // per lane: the next block of the lane's own slots
+                    SEQ_STAT(st, st->v[kStLaneIters]++);
                     const uint4 W = philox_block(bb | (j0 << 20), c1, g0, g1, k0, k1);
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -314,6 +365,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 }
                 // spread: slot p (q-major order) gets lanes [p*L, p*L + L), lane p*L + k tries
                 // word j0 + k
+                SEQ_STAT(st, st->v[kStSpreadIters]++);
                 const int lg1 = C <= 2 ? 5 : (C <= 4 ? 4 : (C <= 8 ? 3 : (C <= 16 ? 2 : 1)));  // L * C <= 64
                 const int L = 1 << lg1;
                 const uint32_t lmask = (uint32_t)((1ull << L) - 1ull);
@@ -348,6 +400,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 j0 += (uint32_t)L;
                 wave_sync();  // tl is rewritten by the next spread
             }
+            SEQ_STAT(st, st->lap(kStCycRetry));
             int val[4];
             bool dup[4];
 #pragma unroll
@@ -364,6 +417,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             }
             int t = min(4 * kWave, xend - base);  // kept: slots base + [x0 - base, t)
             if (__ballot(anyd)) {
+                SEQ_STAT(st, st->v[kStCollRounds]++);
                 // keep the slots below the second-lowest slot of every group of equal picks
                 uint64_t dm[4];
 #pragma unroll
@@ -395,6 +449,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 for (int q = 0; q < 4; ++q)  // ... and redo the kept ones
                     if (act[q] && 4 * lane + q < t) atomicOr(&bm[i[q] >> 5], 1u << (i[q] & 31));
             }
+            SEQ_STAT(st, st->lap(kStCycMark));
             // ring: the lane's four slots in one 16-byte store (base is a multiple of 4); slots
             // below x0 keep their values, slots at or above t are redrawn (and rewritten) before
             // any check that holds them is tested
@@ -415,9 +470,14 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                     if (act[q] && 4 * lane + q < t) out[x] = val[q];
                 }
             }
+            SEQ_STAT(st, st->v[kStKept] += (unsigned long long)(base + t - x0));
             x0 = base + t;
             wave_sync();
-            if (!validate(x0)) { bad = true; return; }
+            if (!validate(x0)) {
+                SEQ_STAT(st, st->v[kStValFail]++);
+                bad = true;
+                return;
+            }
         }
     };
     // compact the unused entries of the stage's pool (R entries), in order, into dst
@@ -453,6 +513,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
         if (cur < 0) rounds(bool_c<false>{}, xend, 0);
         else rounds(bool_c<true>{}, xend, cur);
         if (bad) break;
+        SEQ_STAT(st, st->lap(kStCycRingVal));
         if (Rn <= kSeqFinal) {  // the last entries go to LDS
             if (cur < 0) compact(bool_c<false>{}, 0, c.fin);
             else compact(bool_c<true>{}, cur, c.fin);
@@ -466,6 +527,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
         __syncthreads();
         R = Rn;
         seq_clear_bm(bm, (R + 31) >> 5);
+        SEQ_STAT(st, st->lap(kStCycCompact));
     }
     if (bad) return false;
     // last R <= kSeqFinal entries (in fin): Fisher-Yates by lane 0, then the last slots
@@ -565,11 +627,10 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
 // Search pass: finds, for each of G graphs, its first simple attempt -- the attempt the
 // sequential sampler would return -- with the attempts of a graph spread over waves.
 // Persistent single-wave workgroups; ctl (global, zeroed except best): [0] next graph to open,
-// [1] lowest graph that may still be open (a scan hint), best[G] (kSeqNone: none yet, set by
-// the launcher),
+// [1] unused, best[G] (kSeqNone: none yet, set by the launcher),
 // natt[G] (next attempt index to claim).  A wave claims attempts of its home graph until the
 // graph has a simple attempt (then opens the next graph); when every graph is open it helps:
-// it claims the next attempt of some graph still without one.  Every attempt below a graph's
+// it probes for a graph still without one and claims that graph's attempts until it has one.  Every attempt below a graph's
 // final best is claimed and runs to completion (an attempt is abandoned only once best is
 // below it), so best = the lowest simple attempt, exactly the sequential result, for any
 // schedule.  Attempts >= max_attempts are never drawn (best stays kSeqNone).  Pool rows (E
@@ -590,65 +651,83 @@ __global__ __launch_bounds__(kWave) void sample_search_kernel(SampleShape sh, ui
     int32_t *pools = (int)blockIdx.x < G ? scratch_a + (size_t)blockIdx.x * sh.E
                                          : scratch_b + (size_t)(blockIdx.x - G) * sh.E;
     const uint32_t um = (uint32_t)max_attempts;
-    int home = -1;
+    int home = -1;         // the graph whose attempts this wave claims
+    bool helping = false;  // every graph is open: homes are picked among the open ones
+    uint32_t probe = (uint32_t)blockIdx.x * 0x9E3779B9u + 0x7F4A7C15u;
     for (;;) {
-        // claim (graph, attempt): lane 0 for the home graph, the whole wave when helping
+        // claim (graph, attempt) on the home graph (lane 0)
+        const uint64_t t_claim = LDPC_SEQ_STATS ? __builtin_amdgcn_s_memtime() : 0;
         int g = -1, att = 0;
         if (lane == 0) {
             for (;;) {
-                if (home < 0) home = (int)atomicAdd(&ctl[0], 1u);
-                if (home >= G) break;  // every graph is open: help
+                if (home < 0 && !helping) {
+                    home = (int)atomicAdd(&ctl[0], 1u);
+                    if (home >= G) { home = -1; helping = true; }
+                }
+                if (home < 0) break;  // helping without a home: probe below
                 if (__hip_atomic_load(&best[home], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSeqNone) {
                     const uint32_t a = atomicAdd(&natt[home], 1u);
                     if (a < um) { g = home; att = (int)a; break; }
                 }
-                home = -1;  // resolved or out of attempts: open the next graph
+                home = -1;  // resolved or out of attempts
             }
         }
         g = __shfl(g, 0, kWave);
         att = __shfl(att, 0, kWave);
-        home = __shfl(home, 0, kWave);
+        helping = __shfl((int)helping, 0, kWave) != 0;
         if (g < 0) {
-            // help: scan from the hint for graphs without a simple attempt and attempts left;
-            // wave w takes the (w mod count)-th of the first 64 such graphs found
-            uint32_t lo = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bool prefix = true;  // every graph below the current chunk is resolved
-            for (uint32_t cb = lo; cb < (uint32_t)G && g < 0; cb += kWave) {
-                const uint32_t cg = cb + lane;
-                bool open = false;
-                if (cg < (uint32_t)G)
-                    open = __hip_atomic_load(&best[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSeqNone &&
-                           __hip_atomic_load(&natt[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < um;
-                const uint64_t f = __ballot(open);
-                if (f == 0ull) {
-                    if (prefix && lane == 0) atomicMax(&ctl[1], min(cb + kWave, (uint32_t)G));
-                    continue;
+            // help: probe the graphs from a pseudo-random start (wrapping) for one without a
+            // simple attempt and with attempts left -- 256 graphs per step, their loads issued
+            // together -- and make it the home; none anywhere: this wave is done
+            probe = probe * 1664525u + 1013904223u;
+            const uint32_t start = (uint32_t)(((uint64_t)probe * (uint32_t)G) >> 32);
+            int found = -1;
+            for (uint32_t k = 0; k < (uint32_t)G && found < 0; k += 4 * kWave) {
+                bool open[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t off = k + (uint32_t)(u * kWave + lane);
+                    uint32_t cg = start + off;
+                    if (cg >= (uint32_t)G) cg -= (uint32_t)G;
+                    open[u] = off < (uint32_t)G &&
+                              __hip_atomic_load(&best[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSeqNone &&
+                              __hip_atomic_load(&natt[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < um;
                 }
-                prefix = false;
-                const int cnt = __popcll(f);
-                int pickl = (int)(blockIdx.x % (uint32_t)cnt);
-                uint64_t ff = f;
-                for (int s = 0; s < pickl; ++s) ff &= ff - 1;
-                const int src = (int)__builtin_ctzll(ff);
-                int a = -1;
-                if (lane == 0) {
-                    const uint32_t cand = cb + (uint32_t)src;
-                    const uint32_t aa = atomicAdd(&natt[cand], 1u);
-                    if (aa < um) a = (int)aa;
+#pragma unroll
+                for (int u = 0; u < 4 && found < 0; ++u) {
+                    const uint64_t f = __ballot(open[u]);
+                    if (f) {
+                        uint32_t cg = start + k + (uint32_t)(u * kWave) + (uint32_t)__builtin_ctzll(f);
+                        if (cg >= (uint32_t)G) cg -= (uint32_t)G;
+                        found = (int)cg;
+                    }
                 }
-                a = __shfl(a, 0, kWave);
-                if (a >= 0) {
-                    g = (int)(cb + (uint32_t)src);
-                    att = a;
-                }
-                // else: that graph ran out of attempts meanwhile; rescan this chunk
-                else cb -= kWave;
             }
-            if (g < 0) break;  // nothing left to claim anywhere
+            if (found < 0) break;  // nothing left to claim anywhere
+            home = found;
+#if LDPC_SEQ_STATS
+            if (lane == 0) atomicAdd(&g_seq_stats[kStProbes], 1ull);
+#endif
+            continue;
         }
+#if LDPC_SEQ_STATS
+        if (lane == 0) atomicAdd(&g_seq_stats[kStCycClaim], __builtin_amdgcn_s_memtime() - t_claim);
+#else
+        (void)t_claim;
+#endif
         const uint64_t gid = first_graph + (uint64_t)g;
         const SeqCtx c{sh, k0, k1, (uint32_t)gid, (uint32_t)(gid >> 32), mdv, bm, ring, fin, tl};
-        const bool ok = seq_attempt<CSR, false>(c, att, nullptr, pools, &best[g]);
+#if LDPC_SEQ_STATS
+        SeqStats stats;
+        stats.zero();
+        SeqStats *stp = &stats;
+#else
+        SeqStats *stp = nullptr;
+#endif
+        const uint64_t t_att = LDPC_SEQ_STATS ? __builtin_amdgcn_s_memtime() : 0;
+        const bool ok = seq_attempt<CSR, false>(c, att, nullptr, pools, &best[g], stp);
+        SEQ_STAT(stp, stp->lap(kStCycRingVal); stp->v[kStAttempts]++;
+                 stp->v[kStCycAttempt] += __builtin_amdgcn_s_memtime() - t_att; stp->flush());
         if (ok && lane == 0) atomicMin(&best[g], (uint32_t)att);
         __threadfence_block();
         __syncthreads();
@@ -834,6 +913,16 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
     }
     LDPC_SAMPLE(1024, int32_t, false);
 #undef LDPC_SAMPLE
+}
+
+hipError_t seq_stats(uint64_t *out, int reset) {
+    if (!LDPC_SEQ_STATS) return hipErrorNotSupported;
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seq_stats), sizeof(unsigned long long) * kStCount);
+    if (e == hipSuccess && reset) {
+        static const unsigned long long z[kStCount] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_seq_stats), z, sizeof(z));
+    }
+    return e;
 }
 
 hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,

@@ -337,6 +337,16 @@ int ldpc_debug_mc_plan(const uint8_t *frame_error, int64_t num_trials, int64_t n
 int ldpc_debug_loc_variant(const int32_t *check_ptr, const int32_t *check_var, const int32_t *var_ptr,
                            const int32_t *var_slot, int n, int m, int T, int32_t *variant);
 
+/*
+ * Device diagnostics: the sequential-draw sampler's search-pass counters accumulated since
+ * the last reset (out uint64[16]: attempts, aborted attempts, rounds, slots kept, per-lane
+ * retry iterations, spread retry iterations, rounds with a repeated pick, help probes, then
+ * s_memtime cycles: whole attempts, first draws, retries, marking, ring + validation,
+ * compaction, claims; then failed validations).  Only a diagnostics build
+ * (-DLDPC_SEQ_STATS=1) collects them; the product build returns LDPC_EUNSUP.
+ */
+int ldpc_debug_seq_stats(uint64_t *out, int reset);
+
 /* Name of the soft kernel a graph dispatches to (tests / bench); early_stop: 0 fixed count,
  * 1 early stop with posteriors, 2 early stop with hard decisions only (d_post == NULL). */
 const char *ldpc_bp_kernel_name(const ldpc_graph *g, int early_stop);

@@ -32,6 +32,19 @@ __global__ void kern(uint32_t *out, uint64_t *cyc, uint32_t seed) {
             if constexpr (OP == 4) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(x[i]) : "s"(K));
             if constexpr (OP == 5) asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(x[i]) : "s"(K));
             if constexpr (OP == 6) asm volatile("v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96" : "+v"(x[i]) : "s"(K));
+            if constexpr (OP == 8) asm volatile("v_add_f32 %0, %1, %0" : "+v"(x[i]) : "s"(K));
+            if constexpr (OP == 9) {
+                uint64_t p = x[i] | ((uint64_t)x[i] << 32);
+                asm volatile("v_pk_mul_f32 %0, %0, %0" : "+v"(p));
+                x[i] = (uint32_t)p;
+            }
+            if constexpr (OP == 10) asm volatile("v_rcp_f32 %0, %0" : "+v"(x[i]));
+            if constexpr (OP == 11) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x[i]) : "v"(K ^ x[i]));
+            if constexpr (OP == 12) asm volatile("v_exp_f32 %0, %0" : "+v"(x[i]));
+            if constexpr (OP == 13) asm volatile("v_med3_f32 %0, %0, %1, %0" : "+v"(x[i]) : "s"(K));
+            if constexpr (OP == 14) asm volatile("v_fma_f32 %0, %0, %1, %0" : "+v"(x[i]) : "s"(K));
+            if constexpr (OP == 15) asm volatile("v_and_b32 %0, %1, %0" : "+v"(x[i]) : "s"(K));
+            if constexpr (OP == 16) asm volatile("v_mul_f32 %0, %1, %0" : "+v"(x[i]) : "s"(K));
             if constexpr (OP == 7) {  // mad_u64 alone (result kept, no xor)
                 uint64_t p, c;
                 asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p), "=s"(c) : "v"(x[i]), "s"(K));
@@ -79,6 +92,15 @@ int main() {
         run<5>("v_mul_hi_u32_u24", t);
         run<4>("v_xor_b32", t);
         run<6>("v_bitop3_b32 (xor3)", t);
+        run<8>("v_add_f32", t);
+        run<16>("v_mul_f32", t);
+        run<14>("v_fma_f32", t);
+        run<9>("v_pk_mul_f32", t);
+        run<10>("v_rcp_f32", t);
+        run<12>("v_exp_f32", t);
+        run<13>("v_med3_f32", t);
+        run<11>("v_cndmask_b32", t);
+        run<15>("v_and_b32", t);
     }
     return 0;
 }

@@ -155,3 +155,39 @@ def test_cfg5_ensemble_mc_n64800_vs_oracle(torch):
                                "mean_iterations": float(want[3] / want[0])})
     assert 0 < want[1] < T  # both decoded and failed trials at eps = 0.427 (threshold 0.4294; 10 of 64 with these graphs)
     np.testing.assert_array_equal(got, want)
+
+
+def test_ring_cfg3_early_stop_posteriors_100it_vs_oracle(torch):
+    """configs[3]'s code (RSU ring ensemble, n = 20,000, mixed check degrees 5/6) at its 100
+    iterations, sigma = 0.80, syndrome early stop returning posteriors -- bp_loc_kernel's
+    slab-and-replay instantiation on a mixed-degree layout -- against the oracle's early-stop
+    decode on 256 frames: identical decisions and iteration counts on >= 99 % of frames,
+    posteriors of identical frames within the headline tolerances, stopped frames codewords."""
+    from iib_project_ldpc_codes_amd import decoder, ensembles
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    iters, sigma, F = 100, 0.80, 256
+    g = TannerGraph.from_csr(*ensembles.sample_irregular(ensembles.RSU_DL4, 20000, seed=1, deg2="path").to_csr())
+    assert g.kernel_name(early_stop=True) == "bp_loc_kernel"
+    csr = [np.ascontiguousarray(a, np.int32) for a in g.to_csr()]
+    llr = oracle.channel(oracle.CH_AWGN, sigma, 29, 0, g.n, F)
+    post, hard, its = decoder.bp_decode_dev(g, torch.from_numpy(llr).cuda(), iters, "spa", early_stop=True)
+    torch.cuda.synchronize()
+    gp, gh, gi = post.cpu().numpy(), hard.cpu().numpy(), its.cpu().numpy()
+    op, oh, oi = oracle.bp_decode_batch(csr, llr, iters, 0, early_stop=True)
+    same = np.all(gh == oh, axis=1) & (gi == oi)
+    d = np.abs(gp[same].astype(np.float64) - op[same])
+    ref = np.abs(op[same].astype(np.float64))
+    close = d <= POST_ATOL + POST_RTOL * ref
+    cptr, cvar = csr[0], csr[1]
+    stopped = gi < iters
+    par = np.add.reduceat(gh[stopped][:, cvar].astype(np.int64), cptr[:-1], axis=1) & 1
+    stats = {"frames": F, "iterations": iters, "sigma": sigma, "identical_frames_and_its": float(same.mean()),
+             "mean_its_gpu": float(gi.mean()), "mean_its_oracle": float(oi.mean()),
+             "max_its_gpu": int(gi.max()), "post_close_frac": float(close.mean()),
+             "post_max_abs": float(d.max()), "post_max_rel": float((d / np.maximum(ref, 1.0)).max()),
+             "stopped_frames": int(stopped.sum()), "stopped_not_codeword": int(par.any(axis=1).sum())}
+    _dump("ring_cfg3_early_stop_posteriors_100it_parity", stats)
+    assert same.mean() >= 0.99, stats
+    assert stats["stopped_not_codeword"] == 0 and stopped.any(), stats
+    assert close.mean() >= 0.999, stats
+    assert np.all(d <= SAT_ATOL + SAT_RTOL * ref), stats

@@ -1,7 +1,9 @@
 """Early-stop decodes that ask for hard decisions only (post == NULL) run on bp_loc_kernel
 (the stopping iteration's decisions kept in a bit per variable, csrc/ldpc_kernels.hip); the
-posterior-returning early-stop decode stays on bp_lds_kernel / bp_irr_kernel.  Both must give
-what oracle_bp_decode (ldpc_oracle.c) gives with early_stop = 1:
+posterior-returning early-stop decode runs on bp_loc_kernel's slab-and-replay instantiation
+where the message LDS can stage the posteriors (both the (3,6) codes and the ring code here),
+else on bp_lds_kernel / bp_irr_kernel.  Both must give what oracle_bp_decode (ldpc_oracle.c)
+gives with early_stop = 1:
 
 * min-sum (one check class, the (3,6) codes): hard decisions and iteration counts bit-exact;
 * sum-product: iteration counts and hard decisions identical on >= 99 % of frames (the kernel's
