@@ -138,6 +138,14 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
 // per variable into the bitmap's LDS (fb = 0: global CAS, sample_emit_var_side).
 // oracle_sample_regular / oracle_sample_csr restate it bit for bit.
 constexpr int kSeqFinal = 64, kSeqRing = 512;  // ring: a round (256 slots) + the check it completes
+#ifndef LDPC_SEQ_FIRST_WORDS
+#define LDPC_SEQ_FIRST_WORDS 3  // words every slot draws up front (then only ~f^3 of the slots retry)
+#endif
+constexpr int kSeqFirstWords = LDPC_SEQ_FIRST_WORDS;
+#ifndef LDPC_SEQ_LATE_VALIDATE
+#define LDPC_SEQ_LATE_VALIDATE 0  // 1: a round's completed checks are tested during the next round
+#endif
+constexpr bool kSeqLateValidate = LDPC_SEQ_LATE_VALIDATE;
 
 // LDS ordering between the lanes of one wave (LDS instructions of a wave execute in order):
 // a compiler barrier only -- no s_barrier, no wait for the outstanding global stores that a
@@ -254,7 +262,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 if (f != ~0ull) break;
             }
         } else {
-            cend = upto / dc;
+            cend = __builtin_amdgcn_readfirstlane(upto / dc);
         }
         bool b = false;
         for (int cb = cdone; cb < cend; cb += kWave) {
@@ -330,17 +338,37 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             int i[4];
             bool act[4], need[4];
             {
-                const uint4 W = philox_block(bb, c1, g0, g1, k0, k1);
+                // words 0 .. kSeqFirstWords-1 of every slot at once: independent Philox blocks
+                // (instruction-level parallelism for a wave that is mostly waiting) and one LDS
+                // round trip for all their bitmap reads; the first passing word wins
+                uint4 W[kSeqFirstWords];
+#pragma unroll
+                for (int j = 0; j < kSeqFirstWords; ++j)
+                    W[j] = philox_block(bb | ((uint32_t)j << 20), c1, g0, g1, k0, k1);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int x = base + 4 * lane + q;
                     act[q] = x >= x0 && x < xend;
-                    i[q] = try_word(pick4(W, q));
+                    int e[kSeqFirstWords];
+#pragma unroll
+                    for (int j = 0; j < kSeqFirstWords; ++j) e[j] = try_word(pick4(W[j], q));
+                    i[q] = e[kSeqFirstWords - 1];
+#pragma unroll
+                    for (int j = kSeqFirstWords - 2; j >= 0; --j) i[q] = e[j] >= 0 ? e[j] : i[q];
                     need[q] = act[q] && i[q] < 0;
                 }
             }
+            if constexpr (kSeqLateValidate) {
+                // the checks the previous round completed, tested here so that their ring reads
+                // overlap this round's first draws (a failing attempt runs one round longer)
+                if (!validate(x0)) {
+                    SEQ_STAT(st, st->v[kStValFail]++);
+                    bad = true;
+                    return;
+                }
+            }
             SEQ_STAT(st, st->lap(kStCycDraw));
-            uint32_t j0 = 1;  // next word index of every slot still looking
+            uint32_t j0 = kSeqFirstWords;  // next word index of every slot still looking
             for (;;) {
                 uint64_t mq[4];
                 int C = 0;
@@ -439,7 +467,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                                 else lo2 = min(lo2, s1);
                             }
                         }
-                        t = min(t, lo2);
+                        t = __builtin_amdgcn_readfirstlane(min(t, lo2));
                     }
                 }
 #pragma unroll
@@ -455,12 +483,14 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             // any check that holds them is tested
             {
                 int4 *rp = reinterpret_cast<int4 *>(ring + ((base + 4 * lane) & (kSeqRing - 1)));
-                const int4 old = *rp;
-                int4 nv;
-                nv.x = act[0] ? val[0] : old.x;
-                nv.y = act[1] ? val[1] : old.y;
-                nv.z = act[2] ? val[2] : old.z;
-                nv.w = act[3] ? val[3] : old.w;
+                int4 nv = make_int4(val[0], val[1], val[2], val[3]);
+                if (x0 & 3) {  // the first block has slots below x0 (lane 0): keep their values
+                    const int4 old = *rp;
+                    nv.x = act[0] ? nv.x : old.x;
+                    nv.y = act[1] ? nv.y : old.y;
+                    nv.z = act[2] ? nv.z : old.z;
+                    nv.w = act[3] ? nv.w : old.w;
+                }
                 *rp = nv;
             }
             if constexpr (EMIT) {
@@ -471,13 +501,17 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 }
             }
             SEQ_STAT(st, st->v[kStKept] += (unsigned long long)(base + t - x0));
-            x0 = base + t;
+            x0 = __builtin_amdgcn_readfirstlane(base + t);  // uniform: scalar loop control
             wave_sync();
-            if (!validate(x0)) {
+            if (!kSeqLateValidate && !validate(x0)) {
                 SEQ_STAT(st, st->v[kStValFail]++);
                 bad = true;
                 return;
             }
+        }
+        if (kSeqLateValidate && !validate(x0)) {  // the stage's last round
+            SEQ_STAT(st, st->v[kStValFail]++);
+            bad = true;
         }
     };
     // compact the unused entries of the stage's pool (R entries), in order, into dst
@@ -672,9 +706,10 @@ __global__ __launch_bounds__(kWave) void sample_search_kernel(SampleShape sh, ui
                 home = -1;  // resolved or out of attempts
             }
         }
-        g = __shfl(g, 0, kWave);
-        att = __shfl(att, 0, kWave);
-        helping = __shfl((int)helping, 0, kWave) != 0;
+        // lane 0's claim, as wave-uniform (scalar) values
+        g = __builtin_amdgcn_readfirstlane(g);
+        att = __builtin_amdgcn_readfirstlane(att);
+        helping = __builtin_amdgcn_readfirstlane((int)helping) != 0;
         if (g < 0) {
             // help: probe the graphs from a pseudo-random start (wrapping) for one without a
             // simple attempt and with attempts left -- 256 graphs per step, their loads issued
