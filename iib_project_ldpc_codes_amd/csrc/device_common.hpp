@@ -16,14 +16,16 @@ template <bool B> using bool_c = std::integral_constant<bool, B>;
 // subsequence = codeword, offset = 4*g) -> rocrand4 == philox_block(g, 0,
 // cw_lo, cw_hi) under key {seed_lo, seed_hi}).
 // ---------------------------------------------------------------------------
+// One round = two 32x32->64 products (v_mad_u64_u32: high and low word in one instruction)
+// and two three-input XORs (v_bitop3_b32, truth table 0x96): 40 VALU per block.
 __device__ __forceinline__ uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                               uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+        const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
     return make_uint4(c0, c1, c2, c3);
@@ -31,6 +33,68 @@ __device__ __forceinline__ uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t
 
 __device__ __forceinline__ uint32_t pick4(uint4 r, int i) {
     return i == 0 ? r.x : (i == 1 ? r.y : (i == 2 ? r.z : r.w));
+}
+
+// ---------------------------------------------------------------------------
+// Channels: variable v of codeword cw reads word v mod 4 of Philox {v/4, 0, cw_lo, cw_hi}
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float u01(uint32_t x) {
+    return (float)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8f;
+}
+
+struct ChanArgs {
+    int kind;      // LDPC_CH_*
+    float p, p2;   // see oracle_channel
+    uint32_t k0, k1;
+};
+
+// Channel value of variable 4g + i of a codeword from its Philox block r (all-zero codeword).
+__device__ __forceinline__ float chan_soft_word(const ChanArgs &ch, const uint4 &r, int i) {
+    if (ch.kind == 1) return u01(pick4(r, i)) < ch.p ? -ch.p2 : ch.p2;
+    const int h = i >> 1;
+    const float ua = u01(h ? r.z : r.x), ub = u01(h ? r.w : r.y);
+    const float rad = sqrtf(-2.0f * logf(ua));
+    const float ang = 6.28318530717958647692f * ub;
+    const float g = rad * ((i & 1) ? sinf(ang) : cosf(ang));
+    return (1.0f + ch.p * g) * ch.p2;
+}
+
+// Channel value of variable v of codeword cw.
+__device__ __forceinline__ float chan_soft(const ChanArgs &ch, uint64_t cw, int v) {
+    const uint4 r = philox_block((uint32_t)(v >> 2), 0u, (uint32_t)cw, (uint32_t)(cw >> 32), ch.k0, ch.k1);
+    return chan_soft_word(ch, r, v & 3);
+}
+
+// The Philox block of variables 4g .. 4g + 3 of codeword cw (one block serves the four).
+__device__ __forceinline__ uint4 chan_block(const ChanArgs &ch, uint64_t cw, int g) {
+    return philox_block((uint32_t)g, 0u, (uint32_t)cw, (uint32_t)(cw >> 32), ch.k0, ch.k1);
+}
+
+__device__ __forceinline__ uint8_t chan_bec(const ChanArgs &ch, uint64_t cw, int v) {
+    const uint4 r = philox_block((uint32_t)(v >> 2), 0u, (uint32_t)cw, (uint32_t)(cw >> 32), ch.k0, ch.k1);
+    return u01(pick4(r, v & 3)) < ch.p ? 2 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Block reductions (wave64)
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ int wave_sum(int x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
+    return x;
+}
+
+template <int T>
+__device__ __forceinline__ int block_sum(int x, int *red) {
+    x = wave_sum(x);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = x;
+    __syncthreads();
+    int s = 0;
+#pragma unroll
+    for (int w = 0; w < T / kWave; ++w) s += red[w];
+    __syncthreads();
+    return s;
 }
 
 // Exclusive prefix sum over the workgroup (any multiple of 64 threads <= 1024);

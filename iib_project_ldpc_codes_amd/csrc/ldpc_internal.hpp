@@ -199,6 +199,12 @@ hipError_t launch_sample_csr(int n, int m, int E, const int32_t *d_vsock, const 
                              const int32_t *d_vptr, int max_cdeg, int max_vdeg, uint64_t seed, uint64_t first_graph,
                              int G, int32_t *check_var, int32_t *var_slot, int32_t *attempts, int max_attempts,
                              uint32_t *ctl, hipStream_t stream);
+// Frontier-peeling form of the ensemble BEC Monte-Carlo (peel.hip): regular (dv, dc) graphs
+// whose check state fits LDS; hipErrorNotSupported otherwise (launch_mc_bec_ensemble then
+// runs bec_kernel).
+hipError_t launch_mc_bec_peel(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,
+                              float p, uint64_t seed, uint64_t first_cw, int B, int max_iters, int32_t *trial,
+                              int32_t *trial_its, hipStream_t stream);
 // BEC Monte-Carlo where trial b decodes on graph b of (check_lookup, variable_lookup).
 hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,
                                   float p, uint64_t seed, uint64_t first_cw, int B, int max_iters, int32_t *trial,

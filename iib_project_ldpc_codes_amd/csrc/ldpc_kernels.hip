@@ -59,56 +59,6 @@ namespace {
 #ifndef LDPC_CHECK_W64
 #define LDPC_CHECK_W64 0  // check phase writes each pair edge with its own ds_write_b64
 #endif
-__device__ __forceinline__ float u01(uint32_t x) {
-    return (float)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8f;
-}
-
-struct ChanArgs {
-    int kind;      // LDPC_CH_*
-    float p, p2;   // see oracle_channel
-    uint32_t k0, k1;
-};
-
-// Channel value of variable v of codeword cw (all-zero codeword sent).
-__device__ __forceinline__ float chan_soft(const ChanArgs &ch, uint64_t cw, int v) {
-    const uint4 r = philox_block((uint32_t)(v >> 2), 0u, (uint32_t)cw, (uint32_t)(cw >> 32), ch.k0, ch.k1);
-    const int i = v & 3;
-    if (ch.kind == 1) return u01(pick4(r, i)) < ch.p ? -ch.p2 : ch.p2;
-    const int h = i >> 1;
-    const float ua = u01(h ? r.z : r.x), ub = u01(h ? r.w : r.y);
-    const float rad = sqrtf(-2.0f * logf(ua));
-    const float ang = 6.28318530717958647692f * ub;
-    const float g = rad * ((i & 1) ? sinf(ang) : cosf(ang));
-    return (1.0f + ch.p * g) * ch.p2;
-}
-
-__device__ __forceinline__ uint8_t chan_bec(const ChanArgs &ch, uint64_t cw, int v) {
-    const uint4 r = philox_block((uint32_t)(v >> 2), 0u, (uint32_t)cw, (uint32_t)(cw >> 32), ch.k0, ch.k1);
-    return u01(pick4(r, v & 3)) < ch.p ? 2 : 0;
-}
-
-// ---------------------------------------------------------------------------
-// Block reductions (wave64)
-// ---------------------------------------------------------------------------
-
-__device__ __forceinline__ int wave_sum(int x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
-    return x;
-}
-
-template <int T>
-__device__ __forceinline__ int block_sum(int x, int *red) {
-    x = wave_sum(x);
-    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = x;
-    __syncthreads();
-    int s = 0;
-#pragma unroll
-    for (int w = 0; w < T / kWave; ++w) s += red[w];
-    __syncthreads();
-    return s;
-}
-
 // ===========================================================================
 // 1. BEC erasure decoding -- message_passing.c:7-82, bit-exact.
 //
@@ -152,10 +102,15 @@ __global__ __launch_bounds__(T) void bec_kernel(BecArgs a) {
     int init_cnt = 0;
     if (MC) {
         const uint64_t cw = a.first_cw + b;
-        for (int v = tid; v < n; v += T) {
-            const uint8_t x = chan_bec(a.ch, cw, v);
-            mvc[v] = x;
-            init_cnt += (x == 2);
+        for (int g4 = tid; g4 < (n + 3) >> 2; g4 += T) {  // one Philox block per four variables
+            const uint4 r = chan_block(a.ch, cw, g4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (4 * g4 + q >= n) break;
+                const uint8_t x = u01(pick4(r, q)) < a.ch.p ? 2 : 0;  // chan_bec
+                mvc[4 * g4 + q] = x;
+                init_cnt += (x == 2);
+            }
         }
         for (int i = tid; i < iters; i += T) errs[i] = 0;
     } else {
@@ -1731,10 +1686,15 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             for (int i = tid; i <= iters; i += T) curve[i] = 0;
             if constexpr (MSET)
                 for (int i = tid; i < nsw; i += T) syn[i] = 0u;
-            for (int v = tid; v < n; v += T) {
-                const float l = chan_soft(a.ch, cw, v);
-                msg[v] = to_msg<ALGO>(l);
-                err0 += (l < 0.0f);
+            for (int g4 = tid; g4 < (n + 3) >> 2; g4 += T) {  // one Philox block per four variables
+                const uint4 r = chan_block(a.ch, cw, g4);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (4 * g4 + q >= n) break;
+                    const float l = chan_soft_word(a.ch, r, q);
+                    msg[4 * g4 + q] = to_msg<ALGO>(l);
+                    err0 += (l < 0.0f);
+                }
             }
         } else {
             if constexpr (MSET)
@@ -3400,6 +3360,14 @@ hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lo
                                   float p, uint64_t seed, uint64_t first_cw, int B, int max_iters, int32_t *trial,
                                   int32_t *trial_its, hipStream_t stream) {
     if (B <= 0) return hipSuccess;
+#ifndef LDPC_ENS_PEEL
+#define LDPC_ENS_PEEL 1  // ensemble MC on the frontier-peeling decoder (peel.hip) where it fits
+#endif
+    if (LDPC_ENS_PEEL) {
+        const hipError_t e = launch_mc_bec_peel(n, dv, dc, check_lookup, variable_lookup, p, seed, first_cw, B,
+                                                max_iters, trial, trial_its, stream);
+        if (e != hipErrorNotSupported) return e;
+    }
     ldpc_graph g{};
     g.n = n;
     g.m = n * dv / dc;

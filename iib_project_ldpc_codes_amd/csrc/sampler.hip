@@ -391,10 +391,39 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                     ++j0;
                     continue;
                 }
+                if (C <= 2) {  // one or two slots: each gets 64 / C lanes, no LDS exchange
+                    SEQ_STAT(st, st->v[kStSpreadIters]++);
+                    // the two slots in q-major order, as scalars: (lane, q) of A and B
+                    int la = -1, qa = 0, lb = -1, qb = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        uint64_t mm = mq[q];
+                        if (mm && la < 0) { la = (int)__builtin_ctzll(mm); qa = q; mm &= mm - 1; }
+                        if (mm && lb < 0) { lb = (int)__builtin_ctzll(mm); qb = q; }
+                    }
+                    const int L = C == 1 ? kWave : kWave / 2;
+                    const bool hb = lane >= L;  // lanes of slot B
+                    const int own = hb ? lb : la, qq = hb ? qb : qa;
+                    const uint32_t jj = j0 + (uint32_t)(lane & (L - 1));
+                    const uint4 W =
+                        philox_block(((uint32_t)(base >> 2) + (uint32_t)own) | (jj << 20), c1, g0, g1, k0, k1);
+                    const int eh = jj < 1024u ? try_word(pick4(W, qq)) : -1;
+                    const uint64_t okm = __ballot(eh >= 0);
+                    const uint64_t sa = C == 1 ? okm : (okm & 0xFFFFFFFFull), sb = okm >> 32;
+                    const int ea = sa ? __builtin_amdgcn_readlane(eh, (int)__builtin_ctzll(sa)) : -1;
+                    const int eb = (C == 2 && sb) ? __builtin_amdgcn_readlane(eh, 32 + (int)__builtin_ctzll(sb)) : -1;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (q == qa && lane == la && ea >= 0) { i[q] = ea; need[q] = false; }
+                        if (C == 2 && q == qb && lane == lb && eb >= 0) { i[q] = eb; need[q] = false; }
+                    }
+                    j0 += (uint32_t)L;
+                    continue;
+                }
                 // spread: slot p (q-major order) gets lanes [p*L, p*L + L), lane p*L + k tries
                 // word j0 + k
                 SEQ_STAT(st, st->v[kStSpreadIters]++);
-                const int lg1 = C <= 2 ? 5 : (C <= 4 ? 4 : (C <= 8 ? 3 : (C <= 16 ? 2 : 1)));  // L * C <= 64
+                const int lg1 = C <= 4 ? 4 : (C <= 8 ? 3 : (C <= 16 ? 2 : 1));  // L * C <= 64
                 const int L = 1 << lg1;
                 const uint32_t lmask = (uint32_t)((1ull << L) - 1ull);
                 int pos[4];
@@ -446,30 +475,21 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             int t = min(4 * kWave, xend - base);  // kept: slots base + [x0 - base, t)
             if (__ballot(anyd)) {
                 SEQ_STAT(st, st->v[kStCollRounds]++);
-                // keep the slots below the second-lowest slot of every group of equal picks
-                uint64_t dm[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) dm[q] = __ballot(dup[q]);
+                // Slot s of a group of equal picks is invalid iff an earlier slot of the round is in
+                // its group; every group's second-lowest slot s2 is invalid.  The slots that saw
+                // the bit already set are all of a group but its first arrival, so the lowest of
+                // them is <= s2 -- except that it may be the round's first slot s0, which is
+                // always valid (nothing before it): keep the slots below
+                // min over dup-seeing slots s of max(s, s0 + 1) (at most one valid slot more is
+                // redrawn than the minimum; results do not depend on where a round ends)
+                const int s0 = x0 - base;
+                int dmin = 1 << 30;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    while (dm[q]) {
-                        const int ip = __shfl(i[q], (int)__builtin_ctzll(dm[q]), kWave);
-                        int lo1 = 1 << 30, lo2 = 1 << 30;  // the group's two lowest slots
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const uint64_t g = __ballot(act[r] && i[r] == ip);
-                            dm[r] &= ~g;
-                            if (g) {
-                                const int s1 = 4 * (int)__builtin_ctzll(g) + r;
-                                const uint64_t g2 = g & (g - 1);
-                                const int s2 = g2 ? 4 * (int)__builtin_ctzll(g2) + r : 1 << 30;
-                                if (s1 < lo1) { lo2 = min(lo1, s2); lo1 = s1; }
-                                else lo2 = min(lo2, s1);
-                            }
-                        }
-                        t = __builtin_amdgcn_readfirstlane(min(t, lo2));
-                    }
+                    const uint64_t dm = __ballot(dup[q]);
+                    if (dm) dmin = min(dmin, 4 * (int)__builtin_ctzll(dm) + q);
                 }
+                t = min(t, max(dmin, s0 + 1));
 #pragma unroll
                 for (int q = 0; q < 4; ++q)  // undo every pick of the round ...
                     if (act[q] && !dup[q]) atomicAnd(&bm[i[q] >> 5], ~(1u << (i[q] & 31)));
@@ -622,6 +642,7 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
         for (int x = lane; x < E; x += kWave) out[x] = seq_var_of<CSR>(c, x);
     __threadfence_block();
     __syncthreads();
+    if (fb < 0) return;  // the variable side is built by sample_var_side_kernel
     if (fb == 0) {
         sample_emit_var_side(sh, out, vl);
         return;
@@ -646,6 +667,57 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
     for (int v = lane; v < n; v += kWave) {
         int32_t *r = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
         const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
+        for (int x = 1; x < deg; ++x) {
+            const int key = r[x];
+            int y = x - 1;
+            while (y >= 0 && r[y] > key) {
+                r[y + 1] = r[y];
+                --y;
+            }
+            r[y + 1] = key;
+        }
+    }
+}
+
+// Variable side of G sampled graphs (after the emit pass), one 1024-thread workgroup per
+// graph: every slot takes the next occurrence rank of its variable from fb-bit LDS counters
+// (any order), then each row is sorted -- variable_lookup rows ascending as
+// random_code_generator.c:57-62 (regular: check ids; CSR: slot ids).
+template <int T>
+__global__ __launch_bounds__(T) void sample_var_side_kernel(SampleShape sh, const int32_t *check_lookup,
+                                                            int32_t *variable_lookup, int fb) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem);
+    const int n = sh.n, E = sh.E, dv = sh.dv, dc = sh.dc;
+    const bool csr = sh.vsock != nullptr;
+    const int tid = threadIdx.x;
+    const int32_t *out = check_lookup + (size_t)blockIdx.x * E;
+    int32_t *vl = variable_lookup + (size_t)blockIdx.x * E;
+    const int words = (int)(((long)n * fb + 31) >> 5);
+    for (int w = tid; w < words; w += T) cnt[w] = 0u;
+    __syncthreads();
+    const uint32_t fmask = (1u << fb) - 1u;
+    for (int x = tid; x < E; x += T) {
+        const int v = out[x];
+        const uint32_t pos = (uint32_t)v * (uint32_t)fb;
+        const uint32_t old = atomicAdd(&cnt[pos >> 5], 1u << (pos & 31));
+        const int rank = (int)((old >> (pos & 31)) & fmask);
+        if (csr) vl[sh.vptr[v] + rank] = x;
+        else vl[(size_t)v * dv + rank] = x / dc;
+    }
+    __threadfence_block();  // the row stores above, for the sort below (same workgroup)
+    __syncthreads();
+    for (int v = tid; v < n; v += T) {
+        int32_t *r = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
+        const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
+        if (!csr && deg == 3) {
+            int a = r[0], b = r[1], c = r[2];
+            const int lo = min(a, min(b, c)), hi = max(a, max(b, c)), mid = a + b + c - lo - hi;
+            r[0] = lo;
+            r[1] = mid;
+            r[2] = hi;
+            continue;
+        }
         for (int x = 1; x < deg; ++x) {
             const int key = r[x];
             int y = x - 1;
@@ -760,6 +832,7 @@ __global__ __launch_bounds__(kWave) void sample_search_kernel(SampleShape sh, ui
         SeqStats *stp = nullptr;
 #endif
         const uint64_t t_att = LDPC_SEQ_STATS ? __builtin_amdgcn_s_memtime() : 0;
+        (void)t_att;
         const bool ok = seq_attempt<CSR, false>(c, att, nullptr, pools, &best[g], stp);
         SEQ_STAT(stp, stp->lap(kStCycRingVal); stp->v[kStAttempts]++;
                  stp->v[kStCycAttempt] += __builtin_amdgcn_s_memtime() - t_att; stp->flush());
@@ -942,8 +1015,15 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
             if ((e = hipGetLastError()) != hipSuccess) return e;
             start = ctl + 2;
         }
+        // variable side: a wide workgroup per graph after the emit pass when the counters fit
+        const size_t vs_lds = fb ? (size_t)4 * (((long)sh.n * fb + 31) >> 5) : 0;
+        const bool wide = fb && vs_lds <= 160 * 1024;
         hipLaunchKernelGGL(kern, dim3(G), dim3(kWave), lds, stream, sh, k0, k1, first_graph,
-                           check_lookup, variable_lookup, attempts, max_attempts, bw, fbu, mdv, start);
+                           check_lookup, variable_lookup, attempts, max_attempts, bw, wide ? -1 : fbu, mdv, start);
+        if ((e = hipGetLastError()) != hipSuccess || !wide) return e;
+        if ((e = allow_lds(sample_var_side_kernel<1024>, vs_lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL(sample_var_side_kernel<1024>, dim3(G), dim3(1024), vs_lds, stream, sh, check_lookup,
+                           variable_lookup, fb);
         return hipGetLastError();
     }
     LDPC_SAMPLE(1024, int32_t, false);

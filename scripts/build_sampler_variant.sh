@@ -9,7 +9,7 @@ C=iib_project_ldpc_codes_amd/csrc
 mkdir -p build_variants
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Iinclude -I$C "$@" \
   -c $C/sampler.hip -o build_variants/sampler_$name.o
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC $C/build/ldpc_kernels.o build_variants/sampler_$name.o \
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC $C/build/ldpc_kernels.o build_variants/sampler_$name.o $C/build/peel.o \
   $C/build/capi.o $C/build/mc_run.o $C/build/loc_layout.o -Wl,--version-script=$C/exports.map -Wl,-Bsymbolic -ldl \
   -o build_variants/$name.so
 ls -la build_variants/$name.so
