@@ -10,6 +10,7 @@ namespace {
 
 constexpr int kWave = 64;
 template <bool B> using bool_c = std::integral_constant<bool, B>;
+template <int N> using int_c = std::integral_constant<int, N>;
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (the rocRAND philox4x32_10 stream: rocrand_init(seed,

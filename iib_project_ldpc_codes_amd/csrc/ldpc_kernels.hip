@@ -1510,7 +1510,6 @@ __device__ __forceinline__ uint32_t block_count(int pred, uint32_t *flag, int pa
 #define LDPC_LOC_BLOCK_ANY 1  // bp_loc_kernel early stop: block_any (one barrier) for the stop test
 #endif
 
-template <int N> using int_c = std::integral_constant<int, N>;
 
 // DVN0 / DVN1: non-local edges per variable of local slot 0 / 1 (max); ABS0 / ABS1: some
 // variable of that slot has fewer (its absent edges gather the neutral value).

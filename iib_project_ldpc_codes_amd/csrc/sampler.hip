@@ -137,15 +137,19 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
 // The variable side is built with per-variable occurrence counters packed fb bits
 // per variable into the bitmap's LDS (fb = 0: global CAS, sample_emit_var_side).
 // oracle_sample_regular / oracle_sample_csr restate it bit for bit.
-constexpr int kSeqFinal = 64, kSeqRing = 512;  // ring: a round (256 slots) + the check it completes
+constexpr int kSeqFinal = 64, kSeqRing = 1024;  // ring: a round (<= 512 slots) + the check it completes
 #ifndef LDPC_SEQ_FIRST_WORDS
 #define LDPC_SEQ_FIRST_WORDS 3  // words every slot draws up front (then only ~f^3 of the slots retry)
 #endif
 constexpr int kSeqFirstWords = LDPC_SEQ_FIRST_WORDS;
-#ifndef LDPC_SEQ_LATE_VALIDATE
-#define LDPC_SEQ_LATE_VALIDATE 0  // 1: a round's completed checks are tested during the next round
+#ifndef LDPC_SEQ_WIDE_R
+#define LDPC_SEQ_WIDE_R 40000  // pools of at least this many entries draw 512 slots per round
 #endif
-constexpr bool kSeqLateValidate = LDPC_SEQ_LATE_VALIDATE;
+constexpr int kSeqWideR = LDPC_SEQ_WIDE_R;
+#ifndef LDPC_SEQ_SMALLC
+#define LDPC_SEQ_SMALLC 1  // retries of one or two slots without the LDS task exchange
+#endif
+constexpr bool kSeqSmallC = LDPC_SEQ_SMALLC;
 
 // LDS ordering between the lanes of one wave (LDS instructions of a wave execute in order):
 // a compiler barrier only -- no s_barrier, no wait for the outstanding global stores that a
@@ -173,7 +177,7 @@ struct SeqCtx {
     uint32_t k0, k1, g0, g1;
     uint32_t mdv;   // regular: socket / dv as a multiply-high by ceil(2^32 / dv) (0: divide)
     uint32_t *bm;   // [bw] pool bitmap
-    int *ring;      // [kSeqRing] variable of slot x at x % kSeqRing
+    void *ring;     // [kSeqRing] variable of slot x at x % kSeqRing (u16 when n <= 65536, else int)
     int *fin;       // [kSeqFinal] last pool entries
     int *tl;        // [2 * kWave] retry task list (second half: writes of lanes without a task)
 };
@@ -202,7 +206,7 @@ enum SeqStat {
     kStCycAttempt, kStCycDraw, kStCycRetry, kStCycMark, kStCycRingVal, kStCycCompact, kStCycClaim, kStValFail,
     kStCount
 };
-__device__ unsigned long long g_seq_stats[kStCount];
+__device__ unsigned long long g_seq_stats[2 * kStCount];  // search pass, then emit pass
 struct SeqStats {
     unsigned long long v[kStCount];
     uint64_t t;  // last time stamp
@@ -215,10 +219,10 @@ struct SeqStats {
         v[i] += now - t;
         t = now;
     }
-    __device__ void flush() {
+    __device__ void flush(int pass = 0) {
         if ((threadIdx.x & 63) == 0)
             for (int i = 0; i < kStCount; ++i)
-                if (v[i]) atomicAdd(&g_seq_stats[i], v[i]);
+                if (v[i]) atomicAdd(&g_seq_stats[pass * kStCount + i], v[i]);
     }
 };
 #if LDPC_SEQ_STATS
@@ -238,14 +242,14 @@ struct SeqStats {
 // (search): the attempt is abandoned once *best (the lowest simple attempt found by any
 // wave) is below att -- it can no longer be the graph's first simple attempt.
 // Returns true when the attempt drew a simple graph.
-template <bool CSR, bool EMIT>
+template <bool CSR, bool EMIT, typename RT>
 __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *pools, const uint32_t *best,
                             SeqStats *st = nullptr) {
     const int lane = threadIdx.x & 63;
     const int E = c.sh.E, m = c.sh.m, dc = c.sh.dc;
     const uint32_t k0 = c.k0, k1 = c.k1, g0 = c.g0, g1 = c.g1;
     uint32_t *const bm = c.bm;
-    int *const ring = c.ring;
+    RT *const ring = reinterpret_cast<RT *>(c.ring);
     int *const tl = c.tl;
     const uint32_t c1 = kSampleTag | ((uint32_t)att << 2) | 3u;
     int R = E, x0 = 0, cdone = 0, nround = 0;
@@ -269,12 +273,21 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             const int cc = cb + lane;
             if (cc < cend) {
                 const int lo = CSR ? c.sh.cptr[cc] : cc * dc, d = CSR ? c.sh.cptr[cc + 1] - lo : dc;
-                if (!CSR && d == 6) {  // (3,6): three 8-byte reads (lo even: no pair straddles the ring's end)
-                    const int2 *r2 = reinterpret_cast<const int2 *>(ring);
-                    const int2 a = r2[(lo & (kSeqRing - 1)) >> 1], e = r2[((lo + 2) & (kSeqRing - 1)) >> 1],
-                               f = r2[((lo + 4) & (kSeqRing - 1)) >> 1];
-                    const uint32_t v[6] = {(uint32_t)a.x, (uint32_t)a.y, (uint32_t)e.x,
-                                           (uint32_t)e.y, (uint32_t)f.x, (uint32_t)f.y};
+                if (!CSR && d == 6) {  // (3,6): slots in aligned pairs (lo even: no pair straddles the ring's end)
+                    uint32_t v[6];
+#pragma unroll
+                    for (int u = 0; u < 6; u += 2) {
+                        const int p = (lo + u) & (kSeqRing - 1);
+                        if constexpr (sizeof(RT) == 2) {
+                            const uint32_t w = *reinterpret_cast<const uint32_t *>(ring + p);
+                            v[u] = w & 0xFFFFu;
+                            v[u + 1] = w >> 16;
+                        } else {
+                            const int2 w = *reinterpret_cast<const int2 *>(ring + p);
+                            v[u] = (uint32_t)w.x;
+                            v[u + 1] = (uint32_t)w.y;
+                        }
+                    }
                     uint32_t mn = 0xFFFFFFFFu;  // zero iff two slots hold the same variable
 #pragma unroll
                     for (int u = 0; u < 6; ++u)
@@ -284,15 +297,15 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 } else if (d <= 8) {
                     int v[8];
 #pragma unroll
-                    for (int a = 0; a < 8; ++a) v[a] = a < d ? ring[(lo + a) & (kSeqRing - 1)] : -1 - a;
+                    for (int a = 0; a < 8; ++a) v[a] = a < d ? (int)ring[(lo + a) & (kSeqRing - 1)] : -1 - a;
 #pragma unroll
                     for (int a = 0; a < 8; ++a)
 #pragma unroll
                         for (int e = a + 1; e < 8; ++e) b |= v[a] == v[e];
                 } else {
                     for (int a = 0; a < d && !b; ++a) {
-                        const int va = ring[(lo + a) & (kSeqRing - 1)];
-                        for (int e = a + 1; e < d; ++e) b |= va == ring[(lo + e) & (kSeqRing - 1)];
+                        const int va = (int)ring[(lo + a) & (kSeqRing - 1)];
+                        for (int e = a + 1; e < d; ++e) b |= va == (int)ring[(lo + e) & (kSeqRing - 1)];
                     }
                 }
             }
@@ -303,9 +316,13 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
 
     // the rounds of one stage (slots x0 .. xend - 1); POOL: the pool is the global row at
     // pools + cur (stage 0: the sockets themselves -- the regular form has no global load in
-    // its rounds, so no round waits on earlier stores)
-    auto rounds = [&](auto pool_tag, int xend, int cur) {
+    // its rounds, so no round waits on earlier stores).  NB: Philox blocks per lane per word
+    // index, i.e. up to 256 NB consecutive slots per round -- lane L draws the four slots of
+    // block x0/4 + L + 64 b (b < NB), relative slot 256 b + 4 L + q.
+    auto rounds = [&](auto pool_tag, auto nb_tag, int xend, int cur) {
         constexpr bool POOL = decltype(pool_tag)::value;
+        constexpr int NB = decltype(nb_tag)::value;
+        constexpr int NS = 4 * NB;  // slots per lane
         const int32_t *pool = pools + cur;
         const uint32_t lt = (0u - (uint32_t)R) % (uint32_t)R;  // Lemire: reject low words below this
         // entry of word w, or -1 when Lemire's test or the bitmap rejects it
@@ -315,6 +332,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             const bool used = (bm[e >> 5] >> (e & 31)) & 1u;
             return ((uint32_t)mm < lt || used) ? -1 : e;
         };
+        auto rel = [&](int k, int l) { return 256 * (k >> 2) + 4 * l + (k & 3); };  // slot k of lane l
         while (x0 < xend) {
             if (best && (++nround & 15) == 0) {  // search: a lower simple attempt makes this one moot
                 // (the value loaded 16 rounds ago: the load's latency never stalls a round)
@@ -325,213 +343,219 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 }
                 bseen = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            // lane L: slots 4bb .. 4bb+3 of block bb = x0/4 + L (slots below x0 are done).
+            SEQ_STAT(st, st->v[kStRounds]++; st->lap(kStCycRingVal));
             // Word j of slot x is word x&3 of Philox {x>>2 | j<<20, c1, g}.  A slot takes its
             // first word that passes Lemire's test and whose entry is unused (bitmap of the
-            // slots before the round).  Retries: while many slots still look, every lane draws
-            // the next block of its own four slots; once at most 32 do, the wave spreads them --
-            // L = 2..32 lanes per slot, each trying one of the slot's next L words, the lowest
-            // passing word wins (a slot's words are tried in order, so the result is the same).
-            SEQ_STAT(st, st->v[kStRounds]++; st->lap(kStCycRingVal));
+            // slots before the round).  Every slot first tries words 0 .. kSeqFirstWords-1 at
+            // once (independent Philox blocks: instruction-level parallelism for a wave that is
+            // mostly waiting, and one LDS round trip for their bitmap reads).  Retries: while
+            // many slots still look, every lane draws the next block of its own slots; once at
+            // most 32 do, the wave spreads them -- L = 2..64 lanes per slot, each trying one of
+            // the slot's next L words, the lowest passing word wins (a slot's words are tried in
+            // order, so the result is the same).
             const int base = x0 & ~3;
-            const uint32_t bb = (uint32_t)(base >> 2) + (uint32_t)lane;
-            int i[4];
-            bool act[4], need[4];
-            {
-                // words 0 .. kSeqFirstWords-1 of every slot at once: independent Philox blocks
-                // (instruction-level parallelism for a wave that is mostly waiting) and one LDS
-                // round trip for all their bitmap reads; the first passing word wins
+            uint32_t bb[NB];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) bb[b] = (uint32_t)(base >> 2) + (uint32_t)(lane + 64 * b);
+            int i[NS];
+            bool act[NS], need[NS];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
                 uint4 W[kSeqFirstWords];
 #pragma unroll
                 for (int j = 0; j < kSeqFirstWords; ++j)
-                    W[j] = philox_block(bb | ((uint32_t)j << 20), c1, g0, g1, k0, k1);
+                    W[j] = philox_block(bb[b] | ((uint32_t)j << 20), c1, g0, g1, k0, k1);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const int x = base + 4 * lane + q;
-                    act[q] = x >= x0 && x < xend;
+                    const int k = 4 * b + q, x = base + rel(k, lane);
+                    act[k] = x >= x0 && x < xend;
                     int e[kSeqFirstWords];
 #pragma unroll
                     for (int j = 0; j < kSeqFirstWords; ++j) e[j] = try_word(pick4(W[j], q));
-                    i[q] = e[kSeqFirstWords - 1];
+                    i[k] = e[kSeqFirstWords - 1];
 #pragma unroll
-                    for (int j = kSeqFirstWords - 2; j >= 0; --j) i[q] = e[j] >= 0 ? e[j] : i[q];
-                    need[q] = act[q] && i[q] < 0;
-                }
-            }
-            if constexpr (kSeqLateValidate) {
-                // the checks the previous round completed, tested here so that their ring reads
-                // overlap this round's first draws (a failing attempt runs one round longer)
-                if (!validate(x0)) {
-                    SEQ_STAT(st, st->v[kStValFail]++);
-                    bad = true;
-                    return;
+                    for (int j = kSeqFirstWords - 2; j >= 0; --j) i[k] = e[j] >= 0 ? e[j] : i[k];
+                    need[k] = act[k] && i[k] < 0;
                 }
             }
             SEQ_STAT(st, st->lap(kStCycDraw));
             uint32_t j0 = kSeqFirstWords;  // next word index of every slot still looking
             for (;;) {
-                uint64_t mq[4];
+                uint64_t mq[NS];
                 int C = 0;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    mq[q] = __ballot(need[q]);
-                    C += __popcll(mq[q]);
+                for (int k = 0; k < NS; ++k) {
+                    mq[k] = __ballot(need[k]);
+                    C += __popcll(mq[k]);
                 }
                 if (C == 0) break;
                 if (j0 >= 1024u) { bad = true; return; }  // a slot rejected 1024 words: reject the attempt
                 if (C > 32) {  // per lane: the next block of the lane's own slots
                     SEQ_STAT(st, st->v[kStLaneIters]++);
-                    const uint4 W = philox_block(bb | (j0 << 20), c1, g0, g1, k0, k1);
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int e = try_word(pick4(W, q));
-                        i[q] = need[q] ? e : i[q];
-                        need[q] = need[q] && e < 0;
+                    for (int b = 0; b < NB; ++b) {
+                        const uint4 W = philox_block(bb[b] | (j0 << 20), c1, g0, g1, k0, k1);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const int k = 4 * b + q;
+                            const int e = try_word(pick4(W, q));
+                            i[k] = need[k] ? e : i[k];
+                            need[k] = need[k] && e < 0;
+                        }
                     }
                     ++j0;
                     continue;
                 }
-                if (C <= 2) {  // one or two slots: each gets 64 / C lanes, no LDS exchange
-                    SEQ_STAT(st, st->v[kStSpreadIters]++);
-                    // the two slots in q-major order, as scalars: (lane, q) of A and B
-                    int la = -1, qa = 0, lb = -1, qb = 0;
+                SEQ_STAT(st, st->v[kStSpreadIters]++);
+                if (kSeqSmallC && C <= 2) {  // one or two slots: each gets 64 / C lanes, no LDS exchange
+                    // the two slots (k-major order) as scalars: lane and slot index k of A and B
+                    int la = -1, ka = 0, lb = -1, kb = 0;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        uint64_t mm = mq[q];
-                        if (mm && la < 0) { la = (int)__builtin_ctzll(mm); qa = q; mm &= mm - 1; }
-                        if (mm && lb < 0) { lb = (int)__builtin_ctzll(mm); qb = q; }
+                    for (int k = 0; k < NS; ++k) {
+                        uint64_t mm = mq[k];
+                        if (mm && la < 0) { la = (int)__builtin_ctzll(mm); ka = k; mm &= mm - 1; }
+                        if (mm && lb < 0) { lb = (int)__builtin_ctzll(mm); kb = k; }
                     }
                     const int L = C == 1 ? kWave : kWave / 2;
                     const bool hb = lane >= L;  // lanes of slot B
-                    const int own = hb ? lb : la, qq = hb ? qb : qa;
+                    const int own = hb ? lb : la, kk = hb ? kb : ka;
                     const uint32_t jj = j0 + (uint32_t)(lane & (L - 1));
-                    const uint4 W =
-                        philox_block(((uint32_t)(base >> 2) + (uint32_t)own) | (jj << 20), c1, g0, g1, k0, k1);
-                    const int eh = jj < 1024u ? try_word(pick4(W, qq)) : -1;
+                    const uint32_t ob = (uint32_t)(base >> 2) + (uint32_t)(own + 64 * (kk >> 2));
+                    const uint4 W = philox_block(ob | (jj << 20), c1, g0, g1, k0, k1);
+                    const int eh = jj < 1024u ? try_word(pick4(W, kk & 3)) : -1;
                     const uint64_t okm = __ballot(eh >= 0);
                     const uint64_t sa = C == 1 ? okm : (okm & 0xFFFFFFFFull), sb = okm >> 32;
                     const int ea = sa ? __builtin_amdgcn_readlane(eh, (int)__builtin_ctzll(sa)) : -1;
                     const int eb = (C == 2 && sb) ? __builtin_amdgcn_readlane(eh, 32 + (int)__builtin_ctzll(sb)) : -1;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        if (q == qa && lane == la && ea >= 0) { i[q] = ea; need[q] = false; }
-                        if (C == 2 && q == qb && lane == lb && eb >= 0) { i[q] = eb; need[q] = false; }
+                    for (int k = 0; k < NS; ++k) {
+                        if (k == ka && lane == la && ea >= 0) { i[k] = ea; need[k] = false; }
+                        if (C == 2 && k == kb && lane == lb && eb >= 0) { i[k] = eb; need[k] = false; }
                     }
                     j0 += (uint32_t)L;
                     continue;
                 }
-                // spread: slot p (q-major order) gets lanes [p*L, p*L + L), lane p*L + k tries
-                // word j0 + k
-                SEQ_STAT(st, st->v[kStSpreadIters]++);
+                // spread: slot p (k-major order) gets lanes [p*L, p*L + L), lane p*L + k' tries
+                // word j0 + k'
                 const int lg1 = C <= 4 ? 4 : (C <= 8 ? 3 : (C <= 16 ? 2 : 1));  // L * C <= 64
                 const int L = 1 << lg1;
                 const uint32_t lmask = (uint32_t)((1ull << L) - 1ull);
-                int pos[4];
+                int pos[NS];
                 int pre = 0;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (int k = 0; k < NS; ++k) {
                     const uint32_t below =
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(mq[q] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mq[q], 0u));
-                    pos[q] = pre + (int)below;
-                    pre += __popcll(mq[q]);
-                    tl[need[q] ? pos[q] : kWave + lane] = lane | (q << 6);
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(mq[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mq[k], 0u));
+                    pos[k] = pre + (int)below;
+                    pre += __popcll(mq[k]);
+                    tl[need[k] ? pos[k] : kWave + lane] = lane | (k << 6);
                 }
                 wave_sync();
-                const int p = lane >> lg1, k = lane & (L - 1);
+                const int p = lane >> lg1, kl = lane & (L - 1);
                 const int ent = tl[p < C ? p : 0];
-                const int own = ent & 63, qq = ent >> 6;
-                const uint32_t jj = j0 + (uint32_t)k;
-                const uint4 W = philox_block(((uint32_t)(base >> 2) + (uint32_t)own) | (jj << 20), c1, g0, g1, k0, k1);
-                const int eh = (p < C && jj < 1024u) ? try_word(pick4(W, qq)) : -1;
+                const int own = ent & 63, kk = ent >> 6;
+                const uint32_t jj = j0 + (uint32_t)kl;
+                const uint32_t ob = (uint32_t)(base >> 2) + (uint32_t)(own + 64 * (kk >> 2));
+                const uint4 W = philox_block(ob | (jj << 20), c1, g0, g1, k0, k1);
+                const int eh = (p < C && jj < 1024u) ? try_word(pick4(W, kk & 3)) : -1;
                 const uint64_t okm = __ballot(eh >= 0);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int s0 = need[q] ? pos[q] << lg1 : 0;
+                for (int k = 0; k < NS; ++k) {
+                    const int s0 = need[k] ? pos[k] << lg1 : 0;
                     const uint32_t seg = (uint32_t)(okm >> s0) & lmask;
                     const int src = seg ? s0 + (int)__builtin_ctz(seg) : lane;
                     const int got = __shfl(eh, src, kWave);
-                    const bool hit = need[q] && seg != 0u;
-                    i[q] = hit ? got : i[q];
-                    need[q] = need[q] && seg == 0u;
+                    const bool hit = need[k] && seg != 0u;
+                    i[k] = hit ? got : i[k];
+                    need[k] = need[k] && seg == 0u;
                 }
                 j0 += (uint32_t)L;
                 wave_sync();  // tl is rewritten by the next spread
             }
             SEQ_STAT(st, st->lap(kStCycRetry));
-            int val[4];
-            bool dup[4];
+            int val[NS];
+            bool dup[NS];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                val[q] = 0;
-                if (act[q]) val[q] = POOL ? pool[i[q]] : seq_var_of<CSR>(c, i[q]);
+            for (int k = 0; k < NS; ++k) {
+                val[k] = 0;
+                if (act[k]) val[k] = POOL ? pool[i[k]] : seq_var_of<CSR>(c, i[k]);
             }
             bool anyd = false;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t bit = 1u << (i[q] & 31);
-                dup[q] = act[q] && (atomicOr(&bm[i[q] >> 5], bit) & bit) != 0u;
-                anyd |= dup[q];
+            for (int k = 0; k < NS; ++k) {
+                const uint32_t bit = 1u << (i[k] & 31);
+                dup[k] = act[k] && (atomicOr(&bm[i[k] >> 5], bit) & bit) != 0u;
+                anyd |= dup[k];
             }
-            int t = min(4 * kWave, xend - base);  // kept: slots base + [x0 - base, t)
+            int t = min(256 * NB, xend - base);  // kept: slots base + [x0 - base, t)
             if (__ballot(anyd)) {
                 SEQ_STAT(st, st->v[kStCollRounds]++);
-                // Slot s of a group of equal picks is invalid iff an earlier slot of the round is in
-                // its group; every group's second-lowest slot s2 is invalid.  The slots that saw
-                // the bit already set are all of a group but its first arrival, so the lowest of
-                // them is <= s2 -- except that it may be the round's first slot s0, which is
-                // always valid (nothing before it): keep the slots below
-                // min over dup-seeing slots s of max(s, s0 + 1) (at most one valid slot more is
-                // redrawn than the minimum; results do not depend on where a round ends)
-                const int s0 = x0 - base;
-                int dmin = 1 << 30;
+                // keep the slots below the second-lowest slot of every group of equal picks (the
+                // first invalid slot of the group; which slot saw the bit set depends on the
+                // atomic order, so each group is found from its members' picks)
+                uint64_t dm[NS];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint64_t dm = __ballot(dup[q]);
-                    if (dm) dmin = min(dmin, 4 * (int)__builtin_ctzll(dm) + q);
+                for (int k = 0; k < NS; ++k) dm[k] = __ballot(dup[k]);
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    while (dm[k]) {
+                        const int ip = __shfl(i[k], (int)__builtin_ctzll(dm[k]), kWave);
+                        int lo1 = 1 << 30, lo2 = 1 << 30;  // the group's two lowest slots
+#pragma unroll
+                        for (int r = 0; r < NS; ++r) {
+                            const uint64_t g = __ballot(act[r] && i[r] == ip);
+                            dm[r] &= ~g;
+                            if (g) {
+                                const int s1 = rel(r, (int)__builtin_ctzll(g));
+                                const uint64_t g2 = g & (g - 1);
+                                const int s2 = g2 ? rel(r, (int)__builtin_ctzll(g2)) : 1 << 30;
+                                if (s1 < lo1) { lo2 = min(lo1, s2); lo1 = s1; }
+                                else lo2 = min(lo2, s1);
+                            }
+                        }
+                        t = __builtin_amdgcn_readfirstlane(min(t, lo2));
+                    }
                 }
-                t = min(t, max(dmin, s0 + 1));
 #pragma unroll
-                for (int q = 0; q < 4; ++q)  // undo every pick of the round ...
-                    if (act[q] && !dup[q]) atomicAnd(&bm[i[q] >> 5], ~(1u << (i[q] & 31)));
+                for (int k = 0; k < NS; ++k)  // undo every pick of the round ...
+                    if (act[k] && !dup[k]) atomicAnd(&bm[i[k] >> 5], ~(1u << (i[k] & 31)));
 #pragma unroll
-                for (int q = 0; q < 4; ++q)  // ... and redo the kept ones
-                    if (act[q] && 4 * lane + q < t) atomicOr(&bm[i[q] >> 5], 1u << (i[q] & 31));
+                for (int k = 0; k < NS; ++k)  // ... and redo the kept ones
+                    if (act[k] && rel(k, lane) < t) atomicOr(&bm[i[k] >> 5], 1u << (i[k] & 31));
             }
             SEQ_STAT(st, st->lap(kStCycMark));
-            // ring: the lane's four slots in one 16-byte store (base is a multiple of 4); slots
-            // below x0 keep their values, slots at or above t are redrawn (and rewritten) before
-            // any check that holds them is tested
-            {
-                int4 *rp = reinterpret_cast<int4 *>(ring + ((base + 4 * lane) & (kSeqRing - 1)));
-                int4 nv = make_int4(val[0], val[1], val[2], val[3]);
-                if (x0 & 3) {  // the first block has slots below x0 (lane 0): keep their values
-                    const int4 old = *rp;
-                    nv.x = act[0] ? nv.x : old.x;
-                    nv.y = act[1] ? nv.y : old.y;
-                    nv.z = act[2] ? nv.z : old.z;
-                    nv.w = act[3] ? nv.w : old.w;
+            // ring: each block's four slots in one store (base is a multiple of 4); slots below
+            // x0 keep their values, slots at or above t are redrawn (and rewritten) before any
+            // check that holds them is tested
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const int p = (base + 256 * b + 4 * lane) & (kSeqRing - 1);
+                int nv[4] = {val[4 * b], val[4 * b + 1], val[4 * b + 2], val[4 * b + 3]};
+                if (b == 0 && (x0 & 3)) {  // the first block has slots below x0 (lane 0): keep their values
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) nv[q] = act[q] ? nv[q] : (int)ring[p + q];
                 }
-                *rp = nv;
+                if constexpr (sizeof(RT) == 2)
+                    *reinterpret_cast<uint2 *>(ring + p) =
+                        make_uint2((uint32_t)nv[0] | ((uint32_t)nv[1] << 16), (uint32_t)nv[2] | ((uint32_t)nv[3] << 16));
+                else
+                    *reinterpret_cast<int4 *>(ring + p) = make_int4(nv[0], nv[1], nv[2], nv[3]);
             }
             if constexpr (EMIT) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int x = base + 4 * lane + q;
-                    if (act[q] && 4 * lane + q < t) out[x] = val[q];
+                for (int k = 0; k < NS; ++k) {
+                    const int s = rel(k, lane);
+                    if (act[k] && s < t) out[base + s] = val[k];
                 }
             }
             SEQ_STAT(st, st->v[kStKept] += (unsigned long long)(base + t - x0));
             x0 = __builtin_amdgcn_readfirstlane(base + t);  // uniform: scalar loop control
             wave_sync();
-            if (!kSeqLateValidate && !validate(x0)) {
+            if (!validate(x0)) {
                 SEQ_STAT(st, st->v[kStValFail]++);
                 bad = true;
                 return;
             }
-        }
-        if (kSeqLateValidate && !validate(x0)) {  // the stage's last round
-            SEQ_STAT(st, st->v[kStValFail]++);
-            bad = true;
         }
     };
     // compact the unused entries of the stage's pool (R entries), in order, into dst
@@ -564,8 +588,15 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
     int cur = -1;  // offset of the current pool in `pools` (-1: stage 0, the sockets)
     while (R > kSeqFinal && !bad) {
         const int Rn = (R + 3) >> 2, xend = E - Rn;
-        if (cur < 0) rounds(bool_c<false>{}, xend, 0);
-        else rounds(bool_c<true>{}, xend, cur);
+        // wide rounds (two blocks per lane) while the pool is large: the birthday bound lets
+        // ~400 of 512 slots through a round at R ~ 2e5, ~240 of 256 with one block
+        if (R >= kSeqWideR) {
+            if (cur < 0) rounds(bool_c<false>{}, int_c<2>{}, xend, 0);
+            else rounds(bool_c<true>{}, int_c<2>{}, xend, cur);
+        } else {
+            if (cur < 0) rounds(bool_c<false>{}, int_c<1>{}, xend, 0);
+            else rounds(bool_c<true>{}, int_c<1>{}, xend, cur);
+        }
         if (bad) break;
         SEQ_STAT(st, st->lap(kStCycRingVal));
         if (Rn <= kSeqFinal) {  // the last entries go to LDS
@@ -601,7 +632,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
     if (lane < R) {
         const int x = x0 + lane;
         if constexpr (EMIT) out[x] = fin[lane];
-        ring[x & (kSeqRing - 1)] = fin[lane];
+        ring[x & (kSeqRing - 1)] = (RT)fin[lane];
     }
     wave_sync();
     return validate(E);
@@ -612,7 +643,13 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
 // found by sample_search_kernel, so normally exactly one attempt), writes its slots to
 // check_lookup[g], then builds the variable side.  attempts[g] = attempts drawn from 0
 // (negative: max_attempts without a simple graph -- then the identity configuration).
-template <bool CSR>  // CSR: irregular degree structure (sh.vsock / cptr / vptr)
+// LDS of a sequential-draw wave: bitmap [bw] | fin [kSeqFinal] | tl [2 kWave] | ring [kSeqRing] RT
+template <typename RT>
+__host__ __device__ constexpr size_t seq_lds_bytes(int bw) {
+    return (size_t)4 * (bw + kSeqFinal + 2 * kWave) + sizeof(RT) * kSeqRing;
+}
+
+template <bool CSR, typename RT>  // CSR: irregular degree structure (sh.vsock / cptr / vptr); RT: ring entries
 __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
                                                            uint64_t first_graph, int32_t *check_lookup,
                                                            int32_t *variable_lookup, int32_t *attempts,
@@ -620,9 +657,9 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
                                                            const uint32_t *start) {
     extern __shared__ __align__(16) unsigned char smem[];
     uint32_t *bm = reinterpret_cast<uint32_t *>(smem);  // [bw] pool bitmap, later rank counters
-    int *ring = reinterpret_cast<int *>(bm + bw);       // [kSeqRing]
-    int *fin = ring + kSeqRing;                         // [kSeqFinal]
+    int *fin = reinterpret_cast<int *>(bm + bw);        // [kSeqFinal]
     int *tl = fin + kSeqFinal;                          // [2 * kWave]
+    RT *ring = reinterpret_cast<RT *>(tl + 2 * kWave);  // [kSeqRing]
     const int n = sh.n, E = sh.E, dv = sh.dv, dc = sh.dc;
     constexpr bool csr = CSR;
     const int lane = threadIdx.x;
@@ -634,7 +671,18 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
     int att = start ? (int)min(start[blockIdx.x], (uint32_t)max_attempts) : 0;
     bool ok = false;
     while (!ok && att < max_attempts) {
-        ok = seq_attempt<CSR, true>(c, att, out, vl, nullptr);
+#if LDPC_SEQ_STATS
+        SeqStats stats;
+        stats.zero();
+        const uint64_t t_att = __builtin_amdgcn_s_memtime();
+        ok = seq_attempt<CSR, true, RT>(c, att, out, vl, nullptr, &stats);
+        stats.lap(kStCycRingVal);
+        stats.v[kStAttempts]++;
+        stats.v[kStCycAttempt] += __builtin_amdgcn_s_memtime() - t_att;
+        stats.flush(1);
+#else
+        ok = seq_attempt<CSR, true, RT>(c, att, out, vl, nullptr);
+#endif
         ++att;
     }
     if (attempts && lane == 0) attempts[blockIdx.x] = ok ? att : -att;
@@ -679,48 +727,59 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
     }
 }
 
-// Variable side of G sampled graphs (after the emit pass), one 1024-thread workgroup per
-// graph: every slot takes the next occurrence rank of its variable from fb-bit LDS counters
-// (any order), then each row is sorted -- variable_lookup rows ascending as
-// random_code_generator.c:57-62 (regular: check ids; CSR: slot ids).
-template <int T>
+// Variable side of G sampled graphs (after the emit pass): workgroup (g, k) builds the rows of
+// variables [k V, (k + 1) V) of graph g in LDS -- every slot of the graph whose variable is in
+// the chunk takes the next occurrence rank from fb-bit LDS counters, each row is sorted
+// (variable_lookup rows ascending as random_code_generator.c:57-62; regular: check ids, CSR:
+// slot ids) -- and writes them out in one coalesced pass, instead of E scattered 4-byte stores
+// per graph.  Rows are u16 in LDS when every entry is below 65,536 (so a (3,6) n = 64,800 graph
+// takes three chunks); the chunks of one graph read its check side from L2 / MALL and their
+// workgroup ids share an XCD (ids congruent mod 8).
+template <int T, typename Row>
 __global__ __launch_bounds__(T) void sample_var_side_kernel(SampleShape sh, const int32_t *check_lookup,
-                                                            int32_t *variable_lookup, int fb) {
+                                                            int32_t *variable_lookup, int G, int V, int fb,
+                                                            int maxdeg) {
     extern __shared__ __align__(16) unsigned char smem[];
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem);
     const int n = sh.n, E = sh.E, dv = sh.dv, dc = sh.dc;
     const bool csr = sh.vsock != nullptr;
+    const int nch = (n + V - 1) / V;
+    // id = (g / 8) * 8 * nch + k * gl + g % 8, gl = graphs in g's group of 8
+    const int id = (int)blockIdx.x, grp = id / (8 * nch), rem = id - grp * 8 * nch;
+    const int gl = min(8, G - grp * 8);
+    const int k = rem / gl, g = grp * 8 + rem % gl;
+    const int v0 = k * V, v1 = min(n, v0 + V);
+    const int r0 = csr ? sh.vptr[v0] : v0 * dv, r1 = csr ? sh.vptr[v1] : v1 * dv;
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem);                     // [V * fb bits]
+    Row *rows = reinterpret_cast<Row *>(cnt + ((V * fb + 31) / 32 + 3) / 4 * 4);  // [V * maxdeg]
     const int tid = threadIdx.x;
-    const int32_t *out = check_lookup + (size_t)blockIdx.x * E;
-    int32_t *vl = variable_lookup + (size_t)blockIdx.x * E;
-    const int words = (int)(((long)n * fb + 31) >> 5);
-    for (int w = tid; w < words; w += T) cnt[w] = 0u;
+    const int32_t *out = check_lookup + (size_t)g * E;
+    int32_t *vl = variable_lookup + (size_t)g * E;
+    for (int w = tid; w < (V * fb + 31) / 32; w += T) cnt[w] = 0u;
     __syncthreads();
     const uint32_t fmask = (1u << fb) - 1u;
-    for (int x = tid; x < E; x += T) {
-        const int v = out[x];
-        const uint32_t pos = (uint32_t)v * (uint32_t)fb;
+    auto take = [&](int x, int v) {
+        if (v < v0 || v >= v1) return;
+        const uint32_t pos = (uint32_t)(v - v0) * (uint32_t)fb;
         const uint32_t old = atomicAdd(&cnt[pos >> 5], 1u << (pos & 31));
         const int rank = (int)((old >> (pos & 31)) & fmask);
-        if (csr) vl[sh.vptr[v] + rank] = x;
-        else vl[(size_t)v * dv + rank] = x / dc;
+        rows[(csr ? sh.vptr[v] : v * dv) - r0 + rank] = (Row)(csr ? x : x / dc);
+    };
+    int x = tid;
+    for (; x + 3 * T < E; x += 4 * T) {  // four loads in flight per thread
+        const int va = out[x], vb = out[x + T], vc = out[x + 2 * T], vd = out[x + 3 * T];
+        take(x, va);
+        take(x + T, vb);
+        take(x + 2 * T, vc);
+        take(x + 3 * T, vd);
     }
-    __threadfence_block();  // the row stores above, for the sort below (same workgroup)
+    for (; x < E; x += T) take(x, out[x]);
     __syncthreads();
-    for (int v = tid; v < n; v += T) {
-        int32_t *r = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
+    for (int v = v0 + tid; v < v1; v += T) {
+        Row *r = rows + ((csr ? sh.vptr[v] : v * dv) - r0);
         const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
-        if (!csr && deg == 3) {
-            int a = r[0], b = r[1], c = r[2];
-            const int lo = min(a, min(b, c)), hi = max(a, max(b, c)), mid = a + b + c - lo - hi;
-            r[0] = lo;
-            r[1] = mid;
-            r[2] = hi;
-            continue;
-        }
-        for (int x = 1; x < deg; ++x) {
-            const int key = r[x];
-            int y = x - 1;
+        for (int y0 = 1; y0 < deg; ++y0) {
+            const Row key = r[y0];
+            int y = y0 - 1;
             while (y >= 0 && r[y] > key) {
                 r[y + 1] = r[y];
                 --y;
@@ -728,6 +787,8 @@ __global__ __launch_bounds__(T) void sample_var_side_kernel(SampleShape sh, cons
             r[y + 1] = key;
         }
     }
+    __syncthreads();
+    for (int i = tid; i < r1 - r0; i += T) vl[r0 + i] = (int32_t)rows[i];
 }
 
 // Search pass: finds, for each of G graphs, its first simple attempt -- the attempt the
@@ -742,16 +803,16 @@ __global__ __launch_bounds__(T) void sample_var_side_kernel(SampleShape sh, cons
 // schedule.  Attempts >= max_attempts are never drawn (best stays kSeqNone).  Pool rows (E
 // ints per wave): the rows of the two outputs (grid <= 2G), which the emit pass overwrites;
 // nothing else is written to them -- the emit pass redraws attempt best.
-template <bool CSR>
+template <bool CSR, typename RT>
 __global__ __launch_bounds__(kWave) void sample_search_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
                                                               uint64_t first_graph, int G, int32_t *scratch_a,
                                                               int32_t *scratch_b, uint32_t *ctl, int max_attempts,
                                                               int bw, uint32_t mdv) {
     extern __shared__ __align__(16) unsigned char smem[];
     uint32_t *bm = reinterpret_cast<uint32_t *>(smem);
-    int *ring = reinterpret_cast<int *>(bm + bw);
-    int *fin = ring + kSeqRing;
+    int *fin = reinterpret_cast<int *>(bm + bw);
     int *tl = fin + kSeqFinal;
+    RT *ring = reinterpret_cast<RT *>(tl + 2 * kWave);
     const int lane = threadIdx.x;
     uint32_t *best = ctl + 2, *natt = ctl + 2 + G;
     int32_t *pools = (int)blockIdx.x < G ? scratch_a + (size_t)blockIdx.x * sh.E
@@ -833,7 +894,7 @@ __global__ __launch_bounds__(kWave) void sample_search_kernel(SampleShape sh, ui
 #endif
         const uint64_t t_att = LDPC_SEQ_STATS ? __builtin_amdgcn_s_memtime() : 0;
         (void)t_att;
-        const bool ok = seq_attempt<CSR, false>(c, att, nullptr, pools, &best[g], stp);
+        const bool ok = seq_attempt<CSR, false, RT>(c, att, nullptr, pools, &best[g], stp);
         SEQ_STAT(stp, stp->lap(kStCycRingVal); stp->v[kStAttempts]++;
                  stp->v[kStCycAttempt] += __builtin_amdgcn_s_memtime() - t_att; stp->flush());
         if (ok && lane == 0) atomicMin(&best[g], (uint32_t)att);
@@ -988,8 +1049,10 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
         int bw = ((E + 31) / 32 + 3) & ~3;
         const int fb = max_vdeg <= 3 ? 2 : (max_vdeg <= 15 ? 4 : (max_vdeg <= 255 ? 8 : 0));
         const int fbu = fb && (long)sh.n * fb <= (long)bw * 32 ? fb : 0;
-        const size_t lds = (size_t)4 * (bw + kSeqRing + kSeqFinal + 2 * kWave);
-        auto kern = sh.vsock ? sample_seq_kernel<true> : sample_seq_kernel<false>;
+        const bool r16 = sh.n <= 65536;  // variable ids fit the u16 ring
+        const size_t lds = r16 ? seq_lds_bytes<uint16_t>(bw) : seq_lds_bytes<int>(bw);
+        auto kern = sh.vsock ? (r16 ? sample_seq_kernel<true, uint16_t> : sample_seq_kernel<true, int>)
+                             : (r16 ? sample_seq_kernel<false, uint16_t> : sample_seq_kernel<false, int>);
         hipError_t e = allow_lds(kern, lds);
         if (e != hipSuccess) return e;
         const uint32_t mdv =
@@ -1004,7 +1067,8 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
             if (e != hipSuccess) return e;
             const long per_cu = std::max<long>(1, std::min<long>(32, (long)(160 * 1024) / (long)lds));
             const int W = (int)std::min<long>(2L * G, (long)cus * per_cu);
-            auto sk = sh.vsock ? sample_search_kernel<true> : sample_search_kernel<false>;
+            auto sk = sh.vsock ? (r16 ? sample_search_kernel<true, uint16_t> : sample_search_kernel<true, int>)
+                               : (r16 ? sample_search_kernel<false, uint16_t> : sample_search_kernel<false, int>);
             if ((e = allow_lds(sk, lds)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(ctl, 0, 8, stream)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(ctl + 2, 0xFF, (size_t)4 * G, stream)) != hipSuccess) return e;
@@ -1015,15 +1079,25 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
             if ((e = hipGetLastError()) != hipSuccess) return e;
             start = ctl + 2;
         }
-        // variable side: a wide workgroup per graph after the emit pass when the counters fit
-        const size_t vs_lds = fb ? (size_t)4 * (((long)sh.n * fb + 31) >> 5) : 0;
-        const bool wide = fb && vs_lds <= 160 * 1024;
+        // variable side: chunks of V variables per workgroup after the emit pass, rows of at most
+        // max_vdeg entries staged in LDS (u16 entries when they fit) within ~150 KB
+        const bool u16rows = sh.vsock ? sh.E <= 65536 : sh.m <= 65536;
+        const size_t rb = u16rows ? 2 : 4;
+        int V = 0;
+        if (fb) {
+            const size_t bits = 8 * rb * (size_t)max_vdeg + (size_t)fb;  // LDS bits per variable
+            V = (int)std::min<size_t>((size_t)sh.n, (size_t)150 * 1024 * 8 / bits) & ~63;
+            if (V < 64) V = 0;
+        }
         hipLaunchKernelGGL(kern, dim3(G), dim3(kWave), lds, stream, sh, k0, k1, first_graph,
-                           check_lookup, variable_lookup, attempts, max_attempts, bw, wide ? -1 : fbu, mdv, start);
-        if ((e = hipGetLastError()) != hipSuccess || !wide) return e;
-        if ((e = allow_lds(sample_var_side_kernel<1024>, vs_lds)) != hipSuccess) return e;
-        hipLaunchKernelGGL(sample_var_side_kernel<1024>, dim3(G), dim3(1024), vs_lds, stream, sh, check_lookup,
-                           variable_lookup, fb);
+                           check_lookup, variable_lookup, attempts, max_attempts, bw, V ? -1 : fbu, mdv, start);
+        if ((e = hipGetLastError()) != hipSuccess || !V) return e;
+        const int nch = (sh.n + V - 1) / V;
+        const size_t vs_lds = (size_t)4 * (((long)V * fb + 31) / 32 + 3) / 4 * 4 + rb * (size_t)V * max_vdeg;
+        auto vk = u16rows ? sample_var_side_kernel<1024, uint16_t> : sample_var_side_kernel<1024, int32_t>;
+        if ((e = allow_lds(vk, vs_lds)) != hipSuccess) return e;
+        hipLaunchKernelGGL(vk, dim3((unsigned)G * nch), dim3(1024), vs_lds, stream, sh, check_lookup, variable_lookup,
+                           G, V, fb, max_vdeg);
         return hipGetLastError();
     }
     LDPC_SAMPLE(1024, int32_t, false);
@@ -1032,9 +1106,9 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
 
 hipError_t seq_stats(uint64_t *out, int reset) {
     if (!LDPC_SEQ_STATS) return hipErrorNotSupported;
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seq_stats), sizeof(unsigned long long) * kStCount);
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seq_stats), sizeof(unsigned long long) * 2 * kStCount);
     if (e == hipSuccess && reset) {
-        static const unsigned long long z[kStCount] = {};
+        static const unsigned long long z[2 * kStCount] = {};
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_seq_stats), z, sizeof(z));
     }
     return e;

@@ -338,11 +338,11 @@ int ldpc_debug_loc_variant(const int32_t *check_ptr, const int32_t *check_var, c
                            const int32_t *var_slot, int n, int m, int T, int32_t *variant);
 
 /*
- * Device diagnostics: the sequential-draw sampler's search-pass counters accumulated since
- * the last reset (out uint64[16]: attempts, aborted attempts, rounds, slots kept, per-lane
- * retry iterations, spread retry iterations, rounds with a repeated pick, help probes, then
- * s_memtime cycles: whole attempts, first draws, retries, marking, ring + validation,
- * compaction, claims; then failed validations).  Only a diagnostics build
+ * Device diagnostics: the sequential-draw sampler's counters accumulated since the last reset,
+ * out uint64[32]: the search pass's 16 (attempts, aborted attempts, rounds, slots kept,
+ * per-lane retry iterations, spread retry iterations, rounds with a repeated pick, help probes,
+ * then s_memtime cycles: whole attempts, first draws, retries, marking, ring + validation,
+ * compaction, claims; then failed validations), then the emit pass's 16.  Only a diagnostics build
  * (-DLDPC_SEQ_STATS=1) collects them; the product build returns LDPC_EUNSUP.
  */
 int ldpc_debug_seq_stats(uint64_t *out, int reset);

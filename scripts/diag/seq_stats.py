@@ -15,7 +15,7 @@ L = _native.lib()
 chk = torch.empty((G, n * 3), dtype=torch.int32, device="cuda")
 var = torch.empty_like(chk)
 att = torch.empty(G, dtype=torch.int32, device="cuda")
-st = (ct.c_uint64 * 16)()
+st = (ct.c_uint64 * 32)()
 s = torch.cuda.current_stream()
 _native.check(L.ldpc_sample_regular_dev(n, 3, 6, 5, 0, G, chk.data_ptr(), var.data_ptr(), att.data_ptr(),
                                         s.cuda_stream), "sample")
@@ -28,7 +28,8 @@ _native.check(L.ldpc_sample_regular_dev(n, 3, 6, 5, G, G, chk.data_ptr(), var.da
 b.record(s)
 torch.cuda.synchronize()
 _native.check(L.ldpc_debug_seq_stats(st, 0), "stats")
-v = list(st)
+v = list(st)[:16]
+emit = list(st)[16:]
 names = ["attempts", "aborted", "rounds", "kept", "lane_iters", "spread_iters", "coll_rounds", "probes",
          "cyc_attempt", "cyc_draw", "cyc_retry", "cyc_mark", "cyc_ringval", "cyc_compact", "cyc_claim", "val_fail"]
 d = dict(zip(names, v))
@@ -46,3 +47,6 @@ tot = sum(d[k] for k in ("cyc_draw", "cyc_retry", "cyc_mark", "cyc_ringval", "cy
 print(f"  cycles per round: total(attempt) {d['cyc_attempt'] / R:.0f}  " + "  ".join(
       f"{k[4:]} {d[k] / R:.0f}" for k in ("cyc_draw", "cyc_retry", "cyc_mark", "cyc_ringval", "cyc_compact")) +
       f"  (sum {tot / R:.0f});  claim cycles per attempt {d['cyc_claim'] / A:.0f}  probes {d['probes']}")
+print(f"  emit pass: attempts {emit[0]}  rounds {emit[2]}  cycles per graph {emit[8] / max(G, 1):.0f}  per round "
+      f"{emit[8] / max(emit[2], 1):.0f} (draw {emit[9] / max(emit[2], 1):.0f} retry {emit[10] / max(emit[2], 1):.0f} "
+      f"mark {emit[11] / max(emit[2], 1):.0f} ringval {emit[12] / max(emit[2], 1):.0f} compact {emit[13] / max(emit[2], 1):.0f})")

@@ -2,8 +2,8 @@
 against the sequential definition it must equal (oracle/ldpc_oracle.c seq_attempt): up to 256
 slots (4 per lane) drawn per round against the bitmap of the slots before the round, picks
 marked by atomic OR in an arbitrary lane order, and -- when slots picked the same pool entry --
-only the slots below min over the slots that saw the entry already marked of max(slot, first
-slot + 1) kept (undo every pick, redo the kept ones).  The word
+only the slots below the second-lowest slot of every such group kept (undo every pick, redo
+the kept ones).  The word
 stream is a stand-in hash (the rule, not Philox, is under test); pools compact at ceil(R/4)
 entries left, the last <= 64 entries are shuffled.  CPU only."""
 import hashlib
@@ -89,9 +89,9 @@ def rounds(E, var, att, order_rng):
                     bm[cand[s]] = 1
             t = min(256, xend - base)
             if any(dup.values()):
-                # keep the slots below min over dup-seeing slots s of max(s, s0 + 1)
-                s0 = x0 - base
-                t = min(t, max(min(s for s in slots if dup[s]), s0 + 1))
+                for p in (s for s in slots if dup[s]):
+                    grp = sorted(s for s in slots if cand[s] == cand[p])
+                    t = min(t, grp[1])
                 for s in slots:
                     if not dup[s]:
                         bm[cand[s]] = 0
