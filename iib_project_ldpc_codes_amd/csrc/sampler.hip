@@ -378,7 +378,17 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                     need[k] = act[k] && i[k] < 0;
                 }
             }
+            // later stages: the pool entries of the first draws are loaded now, so the global
+            // load's latency overlaps the retries and the marking (a retried slot reloads)
+            int pre[NS];
+            if constexpr (POOL) {
+#pragma unroll
+                for (int k = 0; k < NS; ++k) pre[k] = pool[max(i[k], 0)];
+            }
             SEQ_STAT(st, st->lap(kStCycDraw));
+            bool firstok[NS];  // the slot kept its first draw (no retry): pre[k] is its value
+#pragma unroll
+            for (int k = 0; k < NS; ++k) firstok[k] = !need[k];
             uint32_t j0 = kSeqFirstWords;  // next word index of every slot still looking
             for (;;) {
                 uint64_t mq[NS];
@@ -478,7 +488,10 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
                 val[k] = 0;
-                if (act[k]) val[k] = POOL ? pool[i[k]] : seq_var_of<CSR>(c, i[k]);
+                if (act[k]) {
+                    if constexpr (POOL) val[k] = firstok[k] ? pre[k] : pool[i[k]];
+                    else val[k] = seq_var_of<CSR>(c, i[k]);
+                }
             }
             bool anyd = false;
 #pragma unroll

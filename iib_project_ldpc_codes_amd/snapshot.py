@@ -26,10 +26,18 @@ import numpy as np
 VERSION = 1
 
 
+# The device sampler's graph stream (csrc/sampler.hip: which graph trial t gets): a resumed
+# ensemble run must draw its remaining graphs from the stream its first part drew from.
+# Snapshots written before the field existed (round 3) used this same stream.
+SAMPLER_RULE = "one-level-rs<8192<=seq-draw<=393216/philox4x32-10"
+
+
 def graph_fingerprint(graph):
-    """Identity of the code a run decodes: the edge lists' digest, or the ensemble parameters."""
+    """Identity of the code a run decodes: the edge lists' digest, or the ensemble parameters
+    (with the device sampler's stream rule)."""
     if not hasattr(graph, "variable_lookup") and hasattr(graph, "dv"):  # montecarlo._Ensemble
-        return {"kind": "ensemble", "n": int(graph.n), "dv": int(graph.dv), "dc": int(graph.dc)}
+        return {"kind": "ensemble", "n": int(graph.n), "dv": int(graph.dv), "dc": int(graph.dc),
+                "sampler": SAMPLER_RULE}
     h = hashlib.sha1()
     if getattr(graph, "csr", None) is not None:
         for a in graph.csr:
@@ -82,8 +90,11 @@ def restore(mc, snap):
     """Continue `mc` from `snap`: same configuration and seed required.  Rank 0 carries the
     restored counts (the per-round all-reduce sums them in); every rank continues at the
     snapshot's next trial index."""
-    if snap["config"] != config(mc) or snap["seed"] != mc.seed:
-        raise ValueError("snapshot is of a different run configuration or seed")
+    have = json.loads(json.dumps(snap["config"]))
+    if have.get("graph", {}).get("kind") == "ensemble":
+        have["graph"].setdefault("sampler", SAMPLER_RULE)  # pre-field snapshots: the same stream
+    if have != config(mc) or snap["seed"] != mc.seed:
+        raise ValueError("snapshot is of a different run configuration, sampler stream or seed")
     if len(snap["trial_ranges"]) != 1:
         raise ValueError("a merged snapshot cannot be resumed (its trials are not one range)")
     t = mc.torch

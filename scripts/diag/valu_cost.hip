@@ -82,7 +82,35 @@ void run(const char *name, int threads) {
     hipFree(cyc);
 }
 
+// s_memtime ticks per second: a long single-wave loop timed by s_memtime and by HIP events
+__global__ void spin(uint64_t *cyc, uint32_t n) {
+    uint32_t x = threadIdx.x;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (uint32_t i = 0; i < n; ++i) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x) : "s"(i));
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) { cyc[0] = t1 - t0; cyc[1] = x; }
+}
+
 int main() {
+    {
+        uint64_t *cyc;
+        hipMalloc(&cyc, 16);
+        hipEvent_t a, b;
+        hipEventCreate(&a);
+        hipEventCreate(&b);
+        spin<<<1, 64>>>(cyc, 1000);
+        hipDeviceSynchronize();
+        hipEventRecord(a);
+        spin<<<1, 64>>>(cyc, 20000000);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms = 0;
+        hipEventElapsedTime(&ms, a, b);
+        uint64_t h[2];
+        hipMemcpy(h, cyc, 16, hipMemcpyDeviceToHost);
+        printf("s_memtime: %llu ticks in %.3f ms = %.3f GHz (loop of 2e7 v_xor: %.2f ticks per iteration)\n",
+               (unsigned long long)h[0], ms, h[0] / (ms * 1e6), h[0] / 2e7);
+    }
     for (int t : {64, 256, 512, 1024}) {
         run<0>("v_mul_lo_u32", t);
         run<1>("v_mul_hi_u32", t);
