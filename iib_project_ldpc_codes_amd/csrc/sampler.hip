@@ -143,8 +143,8 @@ constexpr int kSeqFinal = 64, kSeqRing = 1024;  // ring: a round (<= 512 slots) 
 #endif
 constexpr int kSeqFirstWords = LDPC_SEQ_FIRST_WORDS;
 #ifndef LDPC_SEQ_WIDE_R
-#define LDPC_SEQ_WIDE_R 40000  // pools of at least this many entries draw 512 slots per round
-#endif
+#define LDPC_SEQ_WIDE_R 0  // > 0: pools of at least this many entries draw 512 slots per round
+#endif                     // (measured slower at n = 64,800: more registers, costlier collisions)
 constexpr int kSeqWideR = LDPC_SEQ_WIDE_R;
 #ifndef LDPC_SEQ_SMALLC
 #define LDPC_SEQ_SMALLC 1  // retries of one or two slots without the LDS task exchange
@@ -243,8 +243,8 @@ struct SeqStats {
 // wave) is below att -- it can no longer be the graph's first simple attempt.
 // Returns true when the attempt drew a simple graph.
 template <bool CSR, bool EMIT, typename RT>
-__device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *pools, const uint32_t *best,
-                            SeqStats *st = nullptr) {
+__device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *pools,
+                                            const uint32_t *best, SeqStats *st = nullptr) {
     const int lane = threadIdx.x & 63;
     const int E = c.sh.E, m = c.sh.m, dc = c.sh.dc;
     const uint32_t k0 = c.k0, k1 = c.k1, g0 = c.g0, g1 = c.g1;
@@ -603,7 +603,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
         const int Rn = (R + 3) >> 2, xend = E - Rn;
         // wide rounds (two blocks per lane) while the pool is large: the birthday bound lets
         // ~400 of 512 slots through a round at R ~ 2e5, ~240 of 256 with one block
-        if (R >= kSeqWideR) {
+        if (kSeqWideR > 0 && R >= kSeqWideR) {
             if (cur < 0) rounds(bool_c<false>{}, int_c<2>{}, xend, 0);
             else rounds(bool_c<true>{}, int_c<2>{}, xend, cur);
         } else {
@@ -667,7 +667,7 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
                                                            uint64_t first_graph, int32_t *check_lookup,
                                                            int32_t *variable_lookup, int32_t *attempts,
                                                            int max_attempts, int bw, int fb, uint32_t mdv,
-                                                           const uint32_t *start) {
+                                                           const uint32_t *start, const uint32_t *homewin) {
     extern __shared__ __align__(16) unsigned char smem[];
     uint32_t *bm = reinterpret_cast<uint32_t *>(smem);  // [bw] pool bitmap, later rank counters
     int *fin = reinterpret_cast<int *>(bm + bw);        // [kSeqFinal]
@@ -683,6 +683,10 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
 
     int att = start ? (int)min(start[blockIdx.x], (uint32_t)max_attempts) : 0;
     bool ok = false;
+    if (homewin && att < max_attempts && homewin[blockIdx.x] == (uint32_t)att) {
+        ok = true;  // the search's home wave drew this attempt into check_lookup[g] already
+        ++att;
+    }
     while (!ok && att < max_attempts) {
 #if LDPC_SEQ_STATS
         SeqStats stats;
@@ -806,16 +810,17 @@ __global__ __launch_bounds__(T) void sample_var_side_kernel(SampleShape sh, cons
 
 // Search pass: finds, for each of G graphs, its first simple attempt -- the attempt the
 // sequential sampler would return -- with the attempts of a graph spread over waves.
-// Persistent single-wave workgroups; ctl (global, zeroed except best): [0] next graph to open,
-// [1] unused, best[G] (kSeqNone: none yet, set by the launcher),
-// natt[G] (next attempt index to claim).  A wave claims attempts of its home graph until the
+// Persistent single-wave workgroups; ctl (global): [0] next graph to open, [1] unused,
+// best[G] (kSeqNone: none yet), natt[G] (next attempt index to claim), homewin[G] (the simple
+// attempt the graph's home wave drew into check_lookup[g], kSeqNone: none).  A wave claims attempts of its home graph until the
 // graph has a simple attempt (then opens the next graph); when every graph is open it helps:
 // it probes for a graph still without one and claims that graph's attempts until it has one.  Every attempt below a graph's
 // final best is claimed and runs to completion (an attempt is abandoned only once best is
 // below it), so best = the lowest simple attempt, exactly the sequential result, for any
 // schedule.  Attempts >= max_attempts are never drawn (best stays kSeqNone).  Pool rows (E
-// ints per wave): the rows of the two outputs (grid <= 2G), which the emit pass overwrites;
-// nothing else is written to them -- the emit pass redraws attempt best.
+// ints per wave): variable_lookup rows (grid <= G), rebuilt by the variable-side pass.  The
+// wave that opens a graph draws its attempts into check_lookup[g] and records a simple one in
+// homewin[g]; the emit pass skips g when homewin[g] == best[g] and redraws attempt best otherwise.
 template <bool CSR, typename RT>
 __global__ __launch_bounds__(kWave) void sample_search_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
                                                               uint64_t first_graph, int G, int32_t *scratch_a,
@@ -827,9 +832,8 @@ __global__ __launch_bounds__(kWave) void sample_search_kernel(SampleShape sh, ui
     int *tl = fin + kSeqFinal;
     RT *ring = reinterpret_cast<RT *>(tl + 2 * kWave);
     const int lane = threadIdx.x;
-    uint32_t *best = ctl + 2, *natt = ctl + 2 + G;
-    int32_t *pools = (int)blockIdx.x < G ? scratch_a + (size_t)blockIdx.x * sh.E
-                                         : scratch_b + (size_t)(blockIdx.x - G) * sh.E;
+    uint32_t *best = ctl + 2, *natt = ctl + 2 + G, *homewin = ctl + 2 + 2 * G;
+    int32_t *pools = scratch_b + (size_t)blockIdx.x * sh.E;  // grid <= G: variable_lookup row w
     const uint32_t um = (uint32_t)max_attempts;
     int home = -1;         // the graph whose attempts this wave claims
     bool helping = false;  // every graph is open: homes are picked among the open ones
@@ -907,10 +911,18 @@ __global__ __launch_bounds__(kWave) void sample_search_kernel(SampleShape sh, ui
 #endif
         const uint64_t t_att = LDPC_SEQ_STATS ? __builtin_amdgcn_s_memtime() : 0;
         (void)t_att;
-        const bool ok = seq_attempt<CSR, false, RT>(c, att, nullptr, pools, &best[g], stp);
+        // the wave that opened graph g is the only one writing its check_lookup row: its attempts
+        // draw into it (a simple one is then the graph itself unless a helper's lower attempt wins
+        // -- the emit pass redraws exactly those graphs); helpers only search
+        const bool solo = !helping;
+        const bool ok = solo ? seq_attempt<CSR, true, RT>(c, att, scratch_a + (size_t)g * sh.E, pools, &best[g], stp)
+                             : seq_attempt<CSR, false, RT>(c, att, nullptr, pools, &best[g], stp);
         SEQ_STAT(stp, stp->lap(kStCycRingVal); stp->v[kStAttempts]++;
                  stp->v[kStCycAttempt] += __builtin_amdgcn_s_memtime() - t_att; stp->flush());
-        if (ok && lane == 0) atomicMin(&best[g], (uint32_t)att);
+        if (ok && lane == 0) {
+            atomicMin(&best[g], (uint32_t)att);
+            if (solo) homewin[g] = (uint32_t)att;
+        }
         __threadfence_block();
         __syncthreads();
     }
@@ -1070,7 +1082,7 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
         if (e != hipSuccess) return e;
         const uint32_t mdv =
             sh.vsock == nullptr && sh.dv > 1 && sh.dv < 256 ? (uint32_t)((0x100000000ull + sh.dv - 1) / sh.dv) : 0u;
-        const uint32_t *start = nullptr;
+        const uint32_t *start = nullptr, *homewin = nullptr;
         if (ctl) {
             // search pass: persistent single-wave workgroups, as many as fit the device (LDS
             // bound), at most one pool row each in the 2G rows of the two outputs
@@ -1079,18 +1091,20 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
             if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             if (e != hipSuccess) return e;
             const long per_cu = std::max<long>(1, std::min<long>(32, (long)(160 * 1024) / (long)lds));
-            const int W = (int)std::min<long>(2L * G, (long)cus * per_cu);
+            const int W = (int)std::min<long>((long)G, (long)cus * per_cu);
             auto sk = sh.vsock ? (r16 ? sample_search_kernel<true, uint16_t> : sample_search_kernel<true, int>)
                                : (r16 ? sample_search_kernel<false, uint16_t> : sample_search_kernel<false, int>);
             if ((e = allow_lds(sk, lds)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(ctl, 0, 8, stream)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(ctl + 2, 0xFF, (size_t)4 * G, stream)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(ctl + 2 + G, 0, (size_t)4 * G, stream)) != hipSuccess) return e;
-            // pool rows: wave w < G uses check_lookup row w, wave G + w variable_lookup row w
+            if ((e = hipMemsetAsync(ctl + 2 + 2 * G, 0xFF, (size_t)4 * G, stream)) != hipSuccess) return e;
+            // graphs' home waves draw into check_lookup; pool rows: wave w uses variable_lookup row w
             hipLaunchKernelGGL(sk, dim3(W), dim3(kWave), lds, stream, sh, k0, k1, first_graph, G, check_lookup,
                                variable_lookup, ctl, max_attempts, bw, mdv);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             start = ctl + 2;
+            homewin = ctl + 2 + 2 * G;
         }
         // variable side: chunks of V variables per workgroup after the emit pass, rows of at most
         // max_vdeg entries staged in LDS (u16 entries when they fit) within ~150 KB
@@ -1103,7 +1117,8 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
             if (V < 64) V = 0;
         }
         hipLaunchKernelGGL(kern, dim3(G), dim3(kWave), lds, stream, sh, k0, k1, first_graph,
-                           check_lookup, variable_lookup, attempts, max_attempts, bw, V ? -1 : fbu, mdv, start);
+                           check_lookup, variable_lookup, attempts, max_attempts, bw, V ? -1 : fbu, mdv, start,
+                           homewin);
         if ((e = hipGetLastError()) != hipSuccess || !V) return e;
         const int nch = (sh.n + V - 1) / V;
         const size_t vs_lds = (size_t)4 * (((long)V * fb + 31) / 32 + 3) / 4 * 4 + rb * (size_t)V * max_vdeg;
