@@ -80,10 +80,17 @@ __device__ __forceinline__ uint8_t chan_bec(const ChanArgs &ch, uint64_t cw, int
 // Block reductions (wave64)
 // ---------------------------------------------------------------------------
 
+// Sum over the (fully active) wave as a wave-uniform value: DPP row shifts 1, 2, 4, 8 leave
+// each 16-lane row's sum in its lane 15, row_bcast:15 / :31 fold the rows into lane 63 --
+// full-rate VALU, no LDS round trips or lane-index vectors (the ds_bpermute butterfly's)
 __device__ __forceinline__ int wave_sum(int x) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, kWave);
-    return x;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return __builtin_amdgcn_readlane(x, 63);
 }
 
 template <int T>

@@ -1632,24 +1632,37 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     using HB = std::conditional_t<(4 * KP > 32), uint64_t, uint32_t>;
     static_assert(!MSET || sizeof(HB) == 4, "MSET: 32-bit decision word");
     HB hbits = 0;
-    // MSET: flip the syndrome bits of the checks of var pair v (pair slot k) whose decisions
-    // changed (ch: bit 0 .x, bit 1 .y); b0 / b1: byte addresses of the non-local slots
-    auto syn_flip = [&](auto dn_tag, int k, int ch, const uint32_t (&b0)[DVA], const uint32_t (&b1)[DVA]) {
-        constexpr int DN = decltype(dn_tag)::value;
-        const int q = tid + k * T;
-        if (q >= a.loc_P) return;
+    // MSET: the decisions that changed in a variable phase (chm, bit 2v + h: hbits before XOR
+    // after) flip the syndrome bits of their checks -- the local one (pair q = tid + (v/2) T, bit
+    // 2q + h) and the non-local ones (from the slot's packed LDS positions, re-read from L2).
+    // Each lane walks its own marks after the phase, so the wave loops max-over-lanes times
+    // instead of running a var pair's flips whenever one lane of the wave changed it.
+    uint32_t chm = 0u;
+    auto syn_flush = [&]() {
+        uint32_t mk = chm;
+        chm = 0u;
         const uint32_t P4 = 4u * (uint32_t)a.loc_P;
+        while (__builtin_amdgcn_ballot_w64(mk != 0u)) {
+            if (mk) {
+                const int bit = __builtin_ctz(mk);
+                mk &= mk - 1u;
+                const int v = bit >> 1, h = bit & 1;
+                const int q = tid + (v >> 1) * T;
+                if (q < a.loc_P) {
+                    const uint32_t bl = 2u * (uint32_t)q + (uint32_t)h;
+                    atomicXor(&syn[bl >> 5], 1u << (bl & 31));
+                    const int dn = (v & 1) ? DVN1 : DVN0;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (!((ch >> h) & 1)) continue;
-            const uint32_t bl = 2u * (uint32_t)q + (uint32_t)h;
-            atomicXor(&syn[bl >> 5], 1u << (bl & 31));
-#pragma unroll
-            for (int u = 0; u < DN; ++u) {
-                uint32_t w = ((h ? b1[u] : b0[u]) >> 2) - (uint32_t)lpos0;  // W + r 4P + 4i + 2(row%2) + h'
-                w = w >= P4 ? w - P4 : w;
-                const uint32_t bn = 2u * (w >> 2) + (w & 1u);
-                atomicXor(&syn[bn >> 5], 1u << (bn & 31));
+                    for (int u = 0; u < DVM; ++u) {
+                        if (u < dn) {
+                            const uint32_t spv = (uint32_t)a.loc_pos[(v * DVP + u) * T + tid] + base2;
+                            uint32_t w = ((h ? pos_hi_x4(spv) : pos_lo_x4(spv)) >> 2) - (uint32_t)lpos0;
+                            w = w >= P4 ? w - P4 : w;
+                            const uint32_t bn = 2u * (w >> 2) + (w & 1u);
+                            atomicXor(&syn[bn >> 5], 1u << (bn & 31));
+                        }
+                    }
+                }
             }
         }
     };
@@ -1738,13 +1751,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                 if constexpr (MSET) {  // the channel decisions' syndrome
                     const int d0 = (int)(w.x < 0.0f) | ((int)(w.y < 0.0f) << 1);
                     hbits |= (uint32_t)d0 << (2 * v);
-                    uint32_t b0[DVA], b1[DVA];
-#pragma unroll
-                    for (int u = 0; u < DN; ++u) {
-                        b0[u] = pos_lo_x4(sp[v][u]);
-                        b1[u] = pos_hi_x4(sp[v][u]);
-                    }
-                    if (d0) syn_flip(dn_tag, v >> 1, d0, b0, b1);
+                    chm |= (uint32_t)d0 << (2 * v);
                 }
             }
             loc[v] = w;
@@ -1760,6 +1767,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             init(int_c<DVN0>{}, 2 * k);
             init(int_c<DVN1>{}, 2 * k + 1);
         }
+        if constexpr (MSET) syn_flush();
         // variable phase of var pair v; returns the pair's hard decisions (bit 0: .x, 1: .y)
         auto var_pair = [&](auto dn_tag, auto abs_tag, int v) -> int {
             constexpr int DN = decltype(dn_tag)::value;
@@ -1812,14 +1820,9 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                     at(a1[u]) = s.y - cv[u].y;
                 }
                 loc[v] = make_float2(s.x - loc[v].x, s.y - loc[v].y);
-                if constexpr (MC || ET) dec = (int)(s.x < 0.0f) | ((int)(s.y < 0.0f) << 1);
-                if constexpr (MSET) {
-                    const int ch = dec ^ (int)((hbits >> (2 * v)) & 3u);
-                    if (ch) {
-                        hbits ^= (uint32_t)ch << (2 * v);
-                        syn_flip(dn_tag, v >> 1, ch, a0, a1);
-                    }
-                }
+                // decisions from the sign bits: a min-sum posterior is never -0 (see to_msg)
+                if constexpr (MC || ET)
+                    dec = (int)((__float_as_uint(s.x) >> 31) | ((__float_as_uint(s.y) >> 31) << 1));
             }
             return dec;
         };
@@ -1892,6 +1895,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             if (!MC && it == iters - 1) break;  // the last variable phase only forms posteriors
             // ---- variable phase ----
             int errs = 0;
+            uint32_t nh = 0u;  // MSET: this phase's decisions, bits 2v, 2v + 1
             {
 #pragma unroll
                 for (int k = 0; k < KP; ++k) {
@@ -1899,8 +1903,18 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                     if (LDPC_LOC_VGROUP == 1) __builtin_amdgcn_sched_barrier(0);
                     const int d1 = var_pair(int_c<DVN1>{}, bool_c<ABS1>{}, 2 * k + 1);
                     if (LDPC_LOC_VGROUP > 0) __builtin_amdgcn_sched_barrier(0);
-                    if constexpr (MC) errs += tid + k * T < a.loc_P ? __builtin_popcount(d0) + __builtin_popcount(d1) : 0;
+                    if constexpr (MSET) nh |= (uint32_t)(d0 | d1 << 2) << (4 * k);
+                    else if constexpr (MC) errs += tid + k * T < a.loc_P ? __builtin_popcount(d0) + __builtin_popcount(d1) : 0;
                 }
+            }
+            if constexpr (MSET) {
+                chm = nh ^ (uint32_t)hbits;
+                hbits = nh;
+                if constexpr (MC) {  // pair slots k with tid + k T < P hold variables
+                    const int lim = a.loc_P - tid, nk = lim <= 0 ? 0 : min(KP, (lim + T - 1) / T);
+                    errs = __builtin_popcount(nh & (uint32_t)((1ull << (4 * nk)) - 1ull));
+                }
+                syn_flush();
             }
             if constexpr (MC) {
                 const int w = wave_sum(errs);
