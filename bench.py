@@ -175,7 +175,7 @@ def graph_cfg0():
     return TannerGraph.random_regular(1000, DV, DC, seed=1)
 
 
-ISSUE_PROFILE = os.path.join(ROOT, "profiles", "r03a_issue_model.json")
+ISSUE_PROFILE = os.path.join(ROOT, "profiles", "r04b_issue_model.json")
 SIMDS, CUS, CLOCK_HZ = 1024, 256, 2.4e9
 
 
@@ -250,7 +250,7 @@ def algorithmic_valu_cycles():
 
 
 def load_traffic():
-    for name in ("r03a_pmc_traffic.json", "r02e_pmc_traffic.json", "pmc_traffic.json"):
+    for name in ("r04b_pmc_traffic.json", "r03a_pmc_traffic.json", "pmc_traffic.json"):
         p = os.path.join(ROOT, "profiles", name)
         if os.path.exists(p):
             with open(p) as f:

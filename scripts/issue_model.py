@@ -82,8 +82,10 @@ def loc_parts(bb, T, KP, stats=None):
     assert len(chk) == KP, len(chk)
     # variable phase: the blocks after the check slots holding its 8*KP ds_read_b32 / ds_write_b32
     # (one block; split in ten by the slab-store branches in the early-stop-with-posteriors build)
+    # (searched from the last check slot on, wrapping: the compiler may rotate the loop so the
+    # variable block precedes the check blocks in the code)
     var, nr = [], 0
-    for i in range(chk[-1] + 1, len(bb)):
+    for i in list(range(chk[-1] + 1, len(bb))) + list(range(0, chk[0])):
         ins = bb[i][1]
         if ins.count("ds_read_b32") >= 4 and ins.count("ds_write_b32") >= 4:
             var.append(i)
