@@ -1506,6 +1506,9 @@ __device__ __forceinline__ uint32_t block_count(int pred, uint32_t *flag, int pa
 #ifndef LDPC_LOC_EP_W0
 #define LDPC_LOC_EP_W0 48  // early stop with posteriors: slab writes after syndromes with <= this many threads unsatisfied
 #endif
+#ifndef LDPC_LOC_PERSIST
+#define LDPC_LOC_PERSIST 1  // bp_loc_kernel early stop without posteriors: persistent grid on a counter
+#endif
 #ifndef LDPC_LOC_BLOCK_ANY
 #define LDPC_LOC_BLOCK_ANY 1  // bp_loc_kernel early stop: block_any (one barrier) for the stop test
 #endif
@@ -1680,12 +1683,18 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     static_assert(!EP || (ET && !MC), "EP: early-stop decodes with posteriors");
     constexpr bool ep = EP;
     float2 *slab = ep ? reinterpret_cast<float2 *>(a.scratch) + (size_t)blockIdx.x * VP * T : nullptr;
+    // persistent grid (a.work: EP, and early stop without posteriors when LDPC_LOC_PERSIST):
+    // codewords come from a global counter; thread 0 claims the next one a codeword ahead, so
+    // the atomic's latency hides behind the current decode
     __shared__ int next_b;
+    const bool per = a.work != nullptr;
+    uint32_t claim = 0u;
     for (int round = 0;; ++round) {
-        if (ep && tid == 0) next_b = (int)atomicAdd(a.work, 1u);
+        if (per && tid == 0) next_b = round == 0 ? (int)atomicAdd(a.work, 1u) : (int)claim;
         __syncthreads();  // the previous codeword's outputs are out of LDS; next_b visible
-        const int b = ep ? __builtin_amdgcn_readfirstlane(next_b) : (int)blockIdx.x + round * (int)gridDim.x;
+        const int b = per ? __builtin_amdgcn_readfirstlane(next_b) : (int)blockIdx.x + round * (int)gridDim.x;
         if (b >= a.B) break;
+        if (per && tid == 0) claim = atomicAdd(a.work, 1u);
         const uint64_t cw = a.first_cw + (uint64_t)b;
         int redo_it = -1;  // EP: the variable phase whose slab a second pass must write
     restart:
@@ -3159,7 +3168,13 @@ hipError_t launch_loc_shape(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     auto k = bp_loc_kernel<DLO, DHI, D0, D1, KP, T, ALGO, A0, A1, ET, MC>;
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3(a.B), dim3(T), lds, s, a);
+    unsigned grid = (unsigned)a.B;
+    if (ET && LDPC_LOC_PERSIST && a.scratch) {  // early stop: persistent grid on a codeword counter
+        grid = (unsigned)std::min<int>(a.B, loc_ep_grid());
+        a.work = reinterpret_cast<uint32_t *>(a.scratch);
+        if ((e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, s, a);
     return hipGetLastError();
 }
 
@@ -3296,8 +3311,9 @@ size_t bp_scratch_bytes(const ldpc_graph &g, int B, bool ep_slab) {
     const size_t irr = g.irr_lane && irr_slab(g) ? (size_t)g.irr_P * 4 * (size_t)grid : 0;
     const size_t per = ((size_t)g.E * 5 + (size_t)g.n * 4 + 15) & ~(size_t)15;
     const size_t gen = generic_lds_bytes(g, 0, true) + 4096 <= kLdsMax ? 0 : per * (size_t)grid;
-    // bp_loc_kernel early stop with posteriors: per-workgroup slabs + the codeword counter
-    const size_t loc = ep_slab && g.loc_KP ? loc_ep_slab_floats(g) * 4 + 64 : 0;
+    // bp_loc_kernel early stop: the codeword counter of its persistent grid (+ the per-workgroup
+    // slabs before it when posteriors are asked for)
+    const size_t loc = g.loc_KP ? (ep_slab ? loc_ep_slab_floats(g) * 4 : 0) + 64 : 0;
     return std::max(std::max(irr, gen), loc);
 }
 
