@@ -1507,7 +1507,7 @@ __device__ __forceinline__ uint32_t block_count(int pred, uint32_t *flag, int pa
 #define LDPC_LOC_EP_W0 48  // early stop with posteriors: slab writes after syndromes with <= this many threads unsatisfied
 #endif
 #ifndef LDPC_LOC_PERSIST
-#define LDPC_LOC_PERSIST 1  // bp_loc_kernel early stop without posteriors: persistent grid on a counter
+#define LDPC_LOC_PERSIST 1  // bp_loc_kernel early stop without posteriors: persistent grid on a counter (2: every launch; fixed count +0.4 %, noise)
 #endif
 #ifndef LDPC_LOC_BLOCK_ANY
 #define LDPC_LOC_BLOCK_ANY 1  // bp_loc_kernel early stop: block_any (one barrier) for the stop test
@@ -3169,7 +3169,7 @@ hipError_t launch_loc_shape(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
     unsigned grid = (unsigned)a.B;
-    if (ET && LDPC_LOC_PERSIST && a.scratch) {  // early stop: persistent grid on a codeword counter
+    if ((ET || LDPC_LOC_PERSIST > 1) && LDPC_LOC_PERSIST && a.scratch) {  // persistent grid on a codeword counter
         grid = (unsigned)std::min<int>(a.B, loc_ep_grid());
         a.work = reinterpret_cast<uint32_t *>(a.scratch);
         if ((e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
