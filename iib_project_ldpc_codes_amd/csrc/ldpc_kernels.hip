@@ -940,7 +940,7 @@ struct BpArgs {
     const int32_t *loc_var, *loc_pos, *loc_info;
     int loc_P, loc_ncls, loc_words;
     int loc_cls_q[5], loc_cls_d[4], loc_cls_w[5];
-    uint32_t *work;  // bp_loc_kernel early stop with posteriors: next-codeword counter (zeroed per launch)
+    uint32_t *work;  // bp_loc_kernel early stop (persistent grid): next-codeword counter (zeroed per launch)
 };
 
 // ---------------------------------------------------------------------------
