@@ -146,10 +146,6 @@ constexpr int kSeqFirstWords = LDPC_SEQ_FIRST_WORDS;
 #define LDPC_SEQ_WIDE_R 0  // > 0: pools of at least this many entries draw 512 slots per round
 #endif                     // (measured slower at n = 64,800: more registers, costlier collisions)
 constexpr int kSeqWideR = LDPC_SEQ_WIDE_R;
-#ifndef LDPC_SEQ_SMALLC
-#define LDPC_SEQ_SMALLC 1  // retries of one or two slots without the LDS task exchange
-#endif
-constexpr bool kSeqSmallC = LDPC_SEQ_SMALLC;
 
 // LDS ordering between the lanes of one wave (LDS instructions of a wave execute in order):
 // a compiler barrier only -- no s_barrier, no wait for the outstanding global stores that a
@@ -350,7 +346,7 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
             // once (independent Philox blocks: instruction-level parallelism for a wave that is
             // mostly waiting, and one LDS round trip for their bitmap reads).  Retries: while
             // many slots still look, every lane draws the next block of its own slots; once at
-            // most 32 do, the wave spreads them -- L = 2..64 lanes per slot, each trying one of
+            // most 32 do, the wave spreads them -- L = 2..16 lanes per slot, each trying one of
             // the slot's next L words, the lowest passing word wins (a slot's words are tried in
             // order, so the result is the same).
             const int base = x0 & ~3;
@@ -417,34 +413,6 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
                     continue;
                 }
                 SEQ_STAT(st, st->v[kStSpreadIters]++);
-                if (kSeqSmallC && C <= 2) {  // one or two slots: each gets 64 / C lanes, no LDS exchange
-                    // the two slots (k-major order) as scalars: lane and slot index k of A and B
-                    int la = -1, ka = 0, lb = -1, kb = 0;
-#pragma unroll
-                    for (int k = 0; k < NS; ++k) {
-                        uint64_t mm = mq[k];
-                        if (mm && la < 0) { la = (int)__builtin_ctzll(mm); ka = k; mm &= mm - 1; }
-                        if (mm && lb < 0) { lb = (int)__builtin_ctzll(mm); kb = k; }
-                    }
-                    const int L = C == 1 ? kWave : kWave / 2;
-                    const bool hb = lane >= L;  // lanes of slot B
-                    const int own = hb ? lb : la, kk = hb ? kb : ka;
-                    const uint32_t jj = j0 + (uint32_t)(lane & (L - 1));
-                    const uint32_t ob = (uint32_t)(base >> 2) + (uint32_t)(own + 64 * (kk >> 2));
-                    const uint4 W = philox_block(ob | (jj << 20), c1, g0, g1, k0, k1);
-                    const int eh = jj < 1024u ? try_word(pick4(W, kk & 3)) : -1;
-                    const uint64_t okm = __ballot(eh >= 0);
-                    const uint64_t sa = C == 1 ? okm : (okm & 0xFFFFFFFFull), sb = okm >> 32;
-                    const int ea = sa ? __builtin_amdgcn_readlane(eh, (int)__builtin_ctzll(sa)) : -1;
-                    const int eb = (C == 2 && sb) ? __builtin_amdgcn_readlane(eh, 32 + (int)__builtin_ctzll(sb)) : -1;
-#pragma unroll
-                    for (int k = 0; k < NS; ++k) {
-                        if (k == ka && lane == la && ea >= 0) { i[k] = ea; need[k] = false; }
-                        if (C == 2 && k == kb && lane == lb && eb >= 0) { i[k] = eb; need[k] = false; }
-                    }
-                    j0 += (uint32_t)L;
-                    continue;
-                }
                 // spread: slot p (k-major order) gets lanes [p*L, p*L + L), lane p*L + k' tries
                 // word j0 + k'
                 const int lg1 = C <= 4 ? 4 : (C <= 8 ? 3 : (C <= 16 ? 2 : 1));  // L * C <= 64
