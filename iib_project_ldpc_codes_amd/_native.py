@@ -70,6 +70,8 @@ def lib():
         "ldpc_debug_loc_variant": ([P, P, P, P, i, i, i, P], i),
         "ldpc_debug_mc_plan": ([P, i64, i64, i64, i, i, P], i),
         "ldpc_debug_seq_stats": ([P, i], i),
+        "ldpc_debug_peel_stats": ([P, i], i),
+        "ldpc_debug_peel_cap": ([i], i),
         "ldpc_sample_regular_dev": ([i, i, i, u64, u64, i, P, P, P, P], i),
         "ldpc_sample_regular": ([i, i, i, u64, u64, i, P, P, P], i),
         "ldpc_mc_ensemble_batch_dev": ([i, i, i, i, f, u64, u64, i, i, i, i64, P, P], i),
@@ -109,4 +111,4 @@ def exported_symbols():
             "ldpc_sample_regular", "ldpc_mc_ensemble_batch_dev", "ldpc_ml_decode_batch_dev", "ldpc_ml_decode_batch",
             "ldpc_ml_ensemble_decode_dev", "ldpc_mc_ml_batch_dev", "ldpc_sample_csr_dev", "ldpc_sample_csr",
             "ldpc_mc_run", "ldpc_mc_run_csr", "ldpc_debug_loc_variant", "ldpc_debug_mc_plan",
-            "ldpc_debug_seq_stats"]
+            "ldpc_debug_seq_stats", "ldpc_debug_peel_stats", "ldpc_debug_peel_cap"]

@@ -900,6 +900,19 @@ int ldpc_debug_seq_stats(uint64_t *out, int reset) {
     return LDPC_OK;
 }
 
+int ldpc_debug_peel_stats(uint64_t *out, int reset) {
+    LDPC_REQUIRE(out, "null output");
+    int rc = require_device();
+    if (rc) return rc;
+    LDPC_HIP(peel_stats(out, reset));
+    return LDPC_OK;
+}
+
+int ldpc_debug_peel_cap(int F) {
+    peel_cap(F);
+    return LDPC_OK;
+}
+
 int ldpc_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G, int32_t *check_lookup,
                         int32_t *variable_lookup, int32_t *attempts) {
     int rc = check_regular_shape(n, dv, dc);

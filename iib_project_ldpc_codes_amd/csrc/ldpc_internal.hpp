@@ -205,6 +205,11 @@ hipError_t launch_sample_csr(int n, int m, int E, const int32_t *d_vsock, const 
 hipError_t launch_mc_bec_peel(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,
                               float p, uint64_t seed, uint64_t first_cw, int B, int max_iters, int32_t *trial,
                               int32_t *trial_its, hipStream_t stream);
+// Scan-path evidence of the peeling decoder (device global, this device): [0] overflowed
+// iterations, [1] trials that overflowed, [2] trials decoded.
+hipError_t peel_stats(uint64_t *out, int reset);
+// Test-only cap on the frontier-list capacity (F > 0), 0 restores the LDS budget's capacity.
+void peel_cap(int F);
 // BEC Monte-Carlo where trial b decodes on graph b of (check_lookup, variable_lookup).
 hipError_t launch_mc_bec_ensemble(int n, int dv, int dc, const int32_t *check_lookup, const int32_t *variable_lookup,
                                   float p, uint64_t seed, uint64_t first_cw, int B, int max_iters, int32_t *trial,

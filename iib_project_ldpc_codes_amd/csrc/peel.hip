@@ -21,8 +21,18 @@
 #include "device_common.hpp"
 #include "ldpc_internal.hpp"
 
+#include <atomic>
+
 namespace ldpc {
 namespace {
+
+// Scan-path evidence, always on (a few atomics per trial at most): [0] iterations that ran
+// the bitmap-snapshot scan because the frontier list overflowed, [1] trials with at least one
+// such iteration, [2] trials decoded (ldpc_debug_peel_stats).
+__device__ unsigned long long g_peel_stats[3];
+
+// Test-only frontier capacity override (ldpc_debug_peel_cap); 0 = the LDS budget's capacity.
+std::atomic<int> g_peel_cap{0};
 
 struct PeelArgs {
     const int32_t *cvar, *vchk;  // graph b at + b * graph_stride: check-major slots, v's checks
@@ -89,9 +99,15 @@ __global__ __launch_bounds__(T) void bec_peel_kernel(PeelArgs a) {
 
     int cur = initial, it = 0, its = iters, cl = 0;
     bool fill = false;  // stalled: the remaining counts repeat (message_passing.c:16-19)
+    bool scanned = false;
     for (; it < iters; ++it) {
         const int len = ctl[cl], ovf = ctl[2 + cl];
         int resolved = 0;
+        if (ovf && tid == 0) {
+            atomicAdd(&g_peel_stats[0], 1ull);
+            if (!scanned) atomicAdd(&g_peel_stats[1], 1ull);
+            scanned = true;
+        }
         auto process = [&](int c) {
             const uint32_t s = st[c];
             if ((s >> 24) != 1u) return;  // resolved meanwhile (its variable was the only erasure)
@@ -139,7 +155,10 @@ __global__ __launch_bounds__(T) void bec_peel_kernel(PeelArgs a) {
     // remaining curve entries: the stall value, or zeros after the break (the reference's
     // errors[] stay 0 there)
     for (int i = it + 1 + tid; i <= iters; i += T) tr[i] = fill ? cur : 0;
-    if (tid == 0) a.its[b] = its;
+    if (tid == 0) {
+        a.its[b] = its;
+        atomicAdd(&g_peel_stats[2], 1ull);
+    }
 }
 
 }  // namespace
@@ -157,7 +176,8 @@ hipError_t launch_mc_bec_peel(int n, int dv, int dc, const int32_t *check_lookup
     if (m > 65536 || dc > 255 || (long)dc * n >= (1L << 24) || peel_lds(n, m, 256) > kBudget)
         return hipErrorNotSupported;
     if (B <= 0) return hipSuccess;
-    const int F = (int)std::min<size_t>((size_t)m, (kBudget - peel_lds(n, m, 0)) / 4);
+    int F = (int)std::min<size_t>((size_t)m, (kBudget - peel_lds(n, m, 0)) / 4);
+    if (const int cap = g_peel_cap.load(); cap > 0) F = std::min(F, cap);
     PeelArgs a;
     a.cvar = check_lookup;
     a.vchk = variable_lookup;
@@ -182,5 +202,16 @@ hipError_t launch_mc_bec_peel(int n, int dv, int dc, const int32_t *check_lookup
     hipLaunchKernelGGL(bec_peel_kernel<1024>, dim3(B), dim3(1024), lds, stream, a);
     return hipGetLastError();
 }
+
+hipError_t peel_stats(uint64_t *out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_peel_stats), sizeof(unsigned long long) * 3);
+    if (e == hipSuccess && reset) {
+        static const unsigned long long z[3] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_peel_stats), z, sizeof(z));
+    }
+    return e;
+}
+
+void peel_cap(int F) { g_peel_cap = F > 0 ? F : 0; }
 
 }  // namespace ldpc

@@ -347,6 +347,23 @@ int ldpc_debug_loc_variant(const int32_t *check_ptr, const int32_t *check_var, c
  */
 int ldpc_debug_seq_stats(uint64_t *out, int reset);
 
+/*
+ * Device diagnostics of the ensemble BEC Monte-Carlo's frontier-peeling decoder
+ * (csrc/peel.hip, the message_passing.c:7-82 semantics for the all-zero codeword), collected
+ * by the product build on the current device since the last reset: out uint64[3] =
+ * {iterations that ran the bitmap-snapshot scan because a frontier list overflowed, trials
+ * with at least one such iteration, trials decoded}.  Evidence that the overflow branch ran
+ * in a given launch.
+ */
+int ldpc_debug_peel_stats(uint64_t *out, int reset);
+
+/*
+ * Test-only: cap the peeling decoder's frontier-list capacity at F entries (F > 0) so the
+ * overflow / scan branch runs deterministically at small n; F <= 0 restores the LDS budget's
+ * capacity (5,266 entries at n = 64,800).  Process-wide; results stay bit-exact for any F.
+ */
+int ldpc_debug_peel_cap(int F);
+
 /* Name of the soft kernel a graph dispatches to (tests / bench); early_stop: 0 fixed count,
  * 1 early stop with posteriors, 2 early stop with hard decisions only (d_post == NULL). */
 const char *ldpc_bp_kernel_name(const ldpc_graph *g, int early_stop);

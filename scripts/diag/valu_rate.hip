@@ -1,0 +1,128 @@
+// VALU issue prices on the whole chip, timed by HIP events (gfx950).  Resolves the round-4
+// contradiction of valu_cost.hip (one workgroup, s_memtime around the loop: 4.2-4.4 cycles
+// per plain wave64 instruction per SIMD at four waves per SIMD, against the 2 the issue model
+// and MI355X_MICROARCH.md use).
+//
+// Grid: 256 x W workgroups of 256 threads (one wave per SIMD per workgroup, so W waves per
+// SIMD when the dispatcher spreads them), every lane runs CHAINS independent chains of one
+// instruction REPS times.  Per-SIMD cycles per wave-instruction =
+//     event_time * clock * 1024 SIMDs / (wave-instructions issued),
+// quoted at the nominal 2.4 GHz and at the in-kernel clock (delta s_memtime / delta
+// s_memrealtime x 100 MHz, median over workgroups).  A one-workgroup run (the old probe's
+// shape) reports the same two clocks, which shows what its s_memtime cycles were.
+//   hipcc -O3 --offload-arch=gfx950 scripts/diag/valu_rate.hip -o /tmp/valu_rate && /tmp/valu_rate
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+#define CHAINS 8
+
+template <int OP>
+__global__ __launch_bounds__(256) void kern(uint32_t *out, uint64_t *stamp, uint32_t seed, int reps) {
+    uint32_t x[CHAINS];
+#pragma unroll
+    for (int i = 0; i < CHAINS; ++i) x[i] = seed * (threadIdx.x + 17 * i) + i;
+    const uint32_t K = 0x3F800001u ^ seed;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (int r = 0; r < reps; ++r) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int i = 0; i < CHAINS; ++i) {
+                if constexpr (OP == 0) asm volatile("v_add_f32 %0, %1, %0" : "+v"(x[i]) : "s"(K));
+                if constexpr (OP == 1) asm volatile("v_fma_f32 %0, %0, %1, %0" : "+v"(x[i]) : "s"(K));
+                if constexpr (OP == 2) {
+                    uint64_t p = x[i] | ((uint64_t)x[i] << 32);
+                    asm volatile("v_pk_mul_f32 %0, %0, %0" : "+v"(p));
+                    x[i] = (uint32_t)p;
+                }
+                if constexpr (OP == 3) asm volatile("v_rcp_f32 %0, %0" : "+v"(x[i]));
+                if constexpr (OP == 4) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(x[i]) : "s"(K));
+                if constexpr (OP == 5) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[i]) : "s"(K));
+                if constexpr (OP == 6) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x[i]) : "v"(K));
+            }
+        }
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t a = 0;
+#pragma unroll
+    for (int i = 0; i < CHAINS; ++i) a ^= x[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a;
+    if (threadIdx.x == 0) {
+        stamp[2 * blockIdx.x] = t1 - t0;
+        stamp[2 * blockIdx.x + 1] = r1 - r0;
+    }
+}
+
+template <int OP>
+void run(const char *name, int blocks, int reps, bool one_wg) {
+    uint32_t *out;
+    uint64_t *stamp;
+    hipMalloc(&out, (size_t)4 * 256 * blocks);
+    hipMalloc(&stamp, (size_t)16 * blocks);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    for (int w = 0; w < 3; ++w) kern<OP><<<blocks, 256>>>(out, stamp, 1 + w, reps);  // warm the clock
+    hipDeviceSynchronize();
+    const int launches = 5;
+    hipEventRecord(a);
+    for (int l = 0; l < launches; ++l) kern<OP><<<blocks, 256>>>(out, stamp, 7 + l, reps);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    std::vector<uint64_t> h((size_t)2 * blocks);
+    hipMemcpy(h.data(), stamp, (size_t)16 * blocks, hipMemcpyDeviceToHost);
+    std::vector<double> clk(blocks), cyc(blocks);
+    for (int i = 0; i < blocks; ++i) {
+        clk[i] = (double)h[2 * i] / (double)h[2 * i + 1] * 0.1;  // GHz: memtime ticks per 100 MHz tick
+        cyc[i] = (double)h[2 * i];
+    }
+    std::sort(clk.begin(), clk.end());
+    std::sort(cyc.begin(), cyc.end());
+    const double ghz = clk[blocks / 2];
+    const double wave_instr = (double)blocks * 4 * reps * 4 * CHAINS;  // 4 waves per workgroup
+    const double s = ms * 1e-3;
+    if (one_wg) {
+        // one workgroup = one wave per SIMD on one CU: cycles per wave-instruction of ONE wave
+        const double per_memtime = cyc[blocks / 2] / ((double)reps * 4 * CHAINS);
+        printf("{\"op\": \"%s\", \"shape\": \"1 workgroup, 1 wave/SIMD\", \"memtime_ghz\": %.3f, "
+               "\"memtime_cycles_per_wave_instr\": %.3f, \"event_cycles_per_wave_instr_at_2.4GHz\": %.3f}\n",
+               name, ghz, per_memtime, s / launches * 2.4e9 / ((double)reps * 4 * CHAINS));
+    } else {
+        const int W = blocks / 256;
+        printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"ms_per_launch\": %.4f, \"memtime_ghz\": %.3f, "
+               "\"simd_cycles_per_wave_instr_at_2.4GHz\": %.3f, \"simd_cycles_per_wave_instr_at_memtime_clock\": %.3f}\n",
+               name, W, ms / launches, ghz, s * 2.4e9 * 1024 / (wave_instr * launches),
+               s * ghz * 1e9 * 1024 / (wave_instr * launches));
+    }
+    fflush(stdout);
+    hipFree(out);
+    hipFree(stamp);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+}
+
+template <int OP>
+void sweep(const char *name) {
+    run<OP>(name, 1, 1 << 14, true);
+    for (int W : {1, 2, 4, 8}) run<OP>(name, 256 * W, 1 << 12, false);
+}
+
+int main() {
+    hipDeviceProp_t p;
+    hipGetDeviceProperties(&p, 0);
+    printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d}\n", p.gcnArchName, p.multiProcessorCount, p.clockRate);
+    sweep<0>("v_add_f32");
+    sweep<1>("v_fma_f32");
+    sweep<2>("v_pk_mul_f32");
+    sweep<3>("v_rcp_f32");
+    sweep<4>("v_xor_b32");
+    sweep<5>("v_mul_lo_u32");
+    sweep<6>("v_cndmask_b32");
+    return 0;
+}

@@ -1,4 +1,4 @@
-"""Summarise the sampler profile of scripts/r03k_samp_prof.sh (gpurun_out/prof_samp): kernel time
+"""Summarise the sampler profile of scripts/archive/r03k_samp_prof.sh (gpurun_out/prof_samp): kernel time
 from the trace, PMC counters of the sample_seq_kernel launch, per graph and per attempt.
     python scripts/samp_pmc_summary.py gpurun_out/prof_samp G > profiles/<tag>_sampler_pmc.json"""
 import collections
