@@ -740,7 +740,7 @@ int ldpc_bp_decode_batch_dev(const ldpc_graph *g, const float *d_llr, int B, int
     }
     if (B == 0) return LDPC_OK;
     float *scratch = nullptr;
-    const size_t sb = bp_scratch_bytes(*g, B, early_stop && d_post);
+    const size_t sb = bp_scratch_bytes(*g, B, max_iters, algo, early_stop && d_post);
     if (sb) {
         std::lock_guard<std::mutex> lk(g_mu);
         Workspace &ws = workspace(stream);
@@ -784,7 +784,7 @@ int ldpc_bp_decode_batch(const int32_t *variable_to_check_list, const int32_t *c
         int32_t *di = static_cast<int32_t *>(ws.itsb.p);
         rc = 0;
         // scratch taken inside the _dev call (needs the lock released)
-        if (e == hipSuccess) e = ws.scratch.ensure(bp_scratch_bytes(*g, B, early_stop && post));
+        if (e == hipSuccess) e = ws.scratch.ensure(bp_scratch_bytes(*g, B, max_iters, algo, early_stop && post));
         if (B > 0) {
             // no posteriors asked for: early stop may take the hard-decision path (bp_loc_kernel)
             e = launch_bp_decode(*g, dl, B, max_iters, algo, alpha, early_stop, post ? dp : nullptr, dh, di, nullptr,
@@ -851,7 +851,7 @@ int ldpc_mc_batch_dev(const ldpc_graph *g, int channel, float param, uint64_t se
     LDPC_HIP(ws.cutoff.ensure(16));
     float *scratch = nullptr;
     if (channel != LDPC_CH_BEC) {
-        const size_t sb = bp_scratch_bytes(*g, B, false);
+        const size_t sb = bp_scratch_bytes(*g, B, max_iters, algo, false);
         if (sb) {
             LDPC_HIP(ws.scratch.ensure(sb));
             scratch = static_cast<float *>(ws.scratch.p);

@@ -32,6 +32,74 @@ __device__ __forceinline__ uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t
     return make_uint4(c0, c1, c2, c3);
 }
 
+// NBK Philox blocks that differ only in the first counter word, computed round by round (the
+// blocks' dependency chains interleave: NBK independent products per step instead of one
+// ten-round chain after another); bit-identical to NBK philox_block calls.
+template <int NBK>
+__device__ __forceinline__ void philox_blocks(const uint32_t (&c0)[NBK], uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint32_t k0, uint32_t k1, uint4 (&out)[NBK]) {
+    uint32_t a[NBK], b[NBK], c[NBK], d[NBK];
+#pragma unroll
+    for (int i = 0; i < NBK; ++i) { a[i] = c0[i]; b[i] = c1; c[i] = c2; d[i] = c3; }
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+#pragma unroll
+        for (int i = 0; i < NBK; ++i) {
+            const uint64_t p0 = (uint64_t)0xD2511F53u * a[i], p1 = (uint64_t)0xCD9E8D57u * c[i];
+            a[i] = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), b[i], k0, 0x96);
+            c[i] = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), d[i], k1, 0x96);
+            b[i] = (uint32_t)p1;
+            d[i] = (uint32_t)p0;
+        }
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+#pragma unroll
+    for (int i = 0; i < NBK; ++i) out[i] = make_uint4(a[i], b[i], c[i], d[i]);
+}
+
+// Philox key schedule held in VGPRs (wave-uniform values the compiler would otherwise keep in
+// 20 SGPRs for the whole kernel -- with the graph sampler's other uniform state that spills
+// SGPRs to VGPR lanes, v_writelane / v_readlane + hazard s_nops in the hot loop).
+struct PhiloxKeys {
+    uint32_t a[10], b[10];
+};
+__device__ __forceinline__ PhiloxKeys philox_keys(uint32_t k0, uint32_t k1) {
+    PhiloxKeys K;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        K.a[r] = k0 + (uint32_t)r * 0x9E3779B9u;
+        K.b[r] = k1 + (uint32_t)r * 0xBB67AE85u;
+        asm volatile("" : "+v"(K.a[r]), "+v"(K.b[r]));  // keep them in VGPRs
+    }
+    return K;
+}
+template <int NBK>
+__device__ __forceinline__ void philox_blocks(const uint32_t (&c0)[NBK], uint32_t c1, uint32_t c2, uint32_t c3,
+                                              const PhiloxKeys &K, uint4 (&out)[NBK]) {
+    uint32_t a[NBK], b[NBK], c[NBK], d[NBK];
+#pragma unroll
+    for (int i = 0; i < NBK; ++i) { a[i] = c0[i]; b[i] = c1; c[i] = c2; d[i] = c3; }
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+#pragma unroll
+        for (int i = 0; i < NBK; ++i) {
+            const uint64_t p0 = (uint64_t)0xD2511F53u * a[i], p1 = (uint64_t)0xCD9E8D57u * c[i];
+            a[i] = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), b[i], K.a[r], 0x96);
+            c[i] = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), d[i], K.b[r], 0x96);
+            b[i] = (uint32_t)p1;
+            d[i] = (uint32_t)p0;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NBK; ++i) out[i] = make_uint4(a[i], b[i], c[i], d[i]);
+}
+__device__ __forceinline__ uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, const PhiloxKeys &K) {
+    const uint32_t cc[1] = {c0};
+    uint4 o[1];
+    philox_blocks<1>(cc, c1, c2, c3, K, o);
+    return o[0];
+}
+
 __device__ __forceinline__ uint32_t pick4(uint4 r, int i) {
     return i == 0 ? r.x : (i == 1 ? r.y : (i == 2 ? r.z : r.w));
 }

@@ -157,7 +157,8 @@ hipError_t launch_bp_decode(const ldpc_graph &g, const float *d_llr, int B, int 
 // Bytes of global scratch launch_bp_decode / launch_mc_decode need for this graph/batch (0
 // when the messages fit in LDS); ep_slab: an early-stop decode that returns posteriors (the
 // local-edge kernel's per-workgroup slabs; no other mode uses them).
-size_t bp_scratch_bytes(const ldpc_graph &g, int B, bool ep_slab);
+// ep: an early-stop decode that returns posteriors (the slabs are sized only if it runs on bp_loc_kernel)
+size_t bp_scratch_bytes(const ldpc_graph &g, int B, int iters, int algo, bool ep);
 
 hipError_t launch_channel(int channel, float p, float p2, uint64_t seed, uint64_t first_cw, int n,
                           int B, void *d_out, hipStream_t stream);

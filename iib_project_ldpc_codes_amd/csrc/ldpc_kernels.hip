@@ -1509,6 +1509,9 @@ __device__ __forceinline__ uint32_t block_count(int pred, uint32_t *flag, int pa
 #ifndef LDPC_LOC_PERSIST
 #define LDPC_LOC_PERSIST 1  // bp_loc_kernel early stop without posteriors: persistent grid on a counter (2: every launch; fixed count +0.4 %, noise)
 #endif
+#ifndef LDPC_LOC_PRIO
+#define LDPC_LOC_PRIO 0  // wave priority experiments (1: variable phase prio 1, 2: check phase, 3: odd workgroups)
+#endif
 #ifndef LDPC_LOC_BLOCK_ANY
 #define LDPC_LOC_BLOCK_ANY 1  // bp_loc_kernel early stop: block_any (one barrier) for the stop test
 #endif
@@ -1687,6 +1690,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     // codewords come from a global counter; thread 0 claims the next one a codeword ahead, so
     // the atomic's latency hides behind the current decode
     __shared__ int next_b;
+    if (LDPC_LOC_PRIO == 3 && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);
     const bool per = a.work != nullptr;
     uint32_t claim = 0u;
     for (int round = 0;; ++round) {
@@ -1855,6 +1859,8 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                 for (int v = 0; v < VP; ++v) asm volatile("" : "+v"(inf[v]));
             }
             // ---- check phase ----
+            if (LDPC_LOC_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+            if (LDPC_LOC_PRIO == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int k = 0; k < KP; ++k) {
                 int q = tid + k * T;
@@ -1907,6 +1913,8 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             }
             if (!MC && it == iters - 1) break;  // the last variable phase only forms posteriors
             // ---- variable phase ----
+            if (LDPC_LOC_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+            if (LDPC_LOC_PRIO == 2) __builtin_amdgcn_s_setprio(0);
             int errs = 0;
             HB nh = 0;  // early stop: this phase's decisions, bits 2v, 2v + 1
             {
@@ -3304,7 +3312,10 @@ hipError_t launch_bec_decode(const ldpc_graph &g, uint8_t *d_words, int B, int m
     return run_bec<false>(g, a, B, stream);
 }
 
-size_t bp_scratch_bytes(const ldpc_graph &g, int B, bool ep_slab) {
+size_t bp_scratch_bytes(const ldpc_graph &g, int B, int iters, int algo, bool ep) {
+    // the per-workgroup posterior slabs only when the early-stop-with-posteriors decode will run
+    // on bp_loc_kernel (choose_path may send it to bp_lds_kernel / bp_irr_kernel instead)
+    const bool ep_slab = ep && g.loc_KP && choose_path(g, iters, true, false, algo, false) == BpPath::Loc;
     const int grid = B < LDPC_GMEM_GRID ? B : LDPC_GMEM_GRID;
     // the irregular kernel's slab (if any) and, for iteration counts that push
     // it off LDS, the generic kernel's: enough for whichever path runs

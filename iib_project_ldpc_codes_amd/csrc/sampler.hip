@@ -146,6 +146,12 @@ constexpr int kSeqFirstWords = LDPC_SEQ_FIRST_WORDS;
 #define LDPC_SEQ_WIDE_R 0  // > 0: pools of at least this many entries draw 512 slots per round
 #endif                     // (measured slower at n = 64,800: more registers, costlier collisions)
 constexpr int kSeqWideR = LDPC_SEQ_WIDE_R;
+#ifndef LDPC_SEQ_LOOKAHEAD
+#define LDPC_SEQ_LOOKAHEAD 0  // 1: each round computes the next round's first-word Philox blocks (see rounds;
+#endif                        // measured 2 % slower at n = 64,800: the search pass is issue-bound)
+#ifndef LDPC_SEQ_VKEYS
+#define LDPC_SEQ_VKEYS 1  // the attempt's Philox key schedule in VGPRs (PhiloxKeys)
+#endif
 
 // LDS ordering between the lanes of one wave (LDS instructions of a wave execute in order):
 // a compiler barrier only -- no s_barrier, no wait for the outstanding global stores that a
@@ -244,6 +250,12 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
     const int lane = threadIdx.x & 63;
     const int E = c.sh.E, m = c.sh.m, dc = c.sh.dc;
     const uint32_t k0 = c.k0, k1 = c.k1, g0 = c.g0, g1 = c.g1;
+#if LDPC_SEQ_VKEYS
+    const PhiloxKeys K = philox_keys(k0, k1);  // the round loop's Philox keys in VGPRs
+#define LDPC_SEQ_KEYS K
+#else
+#define LDPC_SEQ_KEYS k0, k1
+#endif
     uint32_t *const bm = c.bm;
     RT *const ring = reinterpret_cast<RT *>(c.ring);
     int *const tl = c.tl;
@@ -329,6 +341,24 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
             return ((uint32_t)mm < lt || used) ? -1 : e;
         };
         auto rel = [&](int k, int l) { return 256 * (k >> 2) + 4 * l + (k & 3); };  // slot k of lane l
+        // The first words of every slot of the round at base bs: the NB x kSeqFirstWords Philox
+        // blocks of the lane, computed round-interleaved.  Each round computes the NEXT round's
+        // blocks (for base + 256 NB, right after its bitmap atomics are issued, so the ten-step
+        // product chains run in the atomics' / ring's LDS latency); a round whose base differs
+        // (a collision kept fewer slots) recomputes its own.  Words depend only on (slot, j), so
+        // the schedule changes no result.
+        uint4 Wn[NB * kSeqFirstWords];
+        int pbase = -1;
+        auto first_words = [&](int bs) {
+            uint32_t cc[NB * kSeqFirstWords];
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int j = 0; j < kSeqFirstWords; ++j)
+                    cc[b * kSeqFirstWords + j] = ((uint32_t)(bs >> 2) + (uint32_t)(lane + 64 * b)) | ((uint32_t)j << 20);
+            philox_blocks<NB * kSeqFirstWords>(cc, c1, g0, g1, LDPC_SEQ_KEYS, Wn);
+            pbase = bs;
+        };
         while (x0 < xend) {
             if (best && (++nround & 15) == 0) {  // search: a lower simple attempt makes this one moot
                 // (the value loaded 16 rounds ago: the load's latency never stalls a round)
@@ -353,21 +383,18 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
             uint32_t bb[NB];
 #pragma unroll
             for (int b = 0; b < NB; ++b) bb[b] = (uint32_t)(base >> 2) + (uint32_t)(lane + 64 * b);
+            if (base != pbase) first_words(base);  // the last round's look-ahead guessed another base
             int i[NS];
             bool act[NS], need[NS];
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
-                uint4 W[kSeqFirstWords];
-#pragma unroll
-                for (int j = 0; j < kSeqFirstWords; ++j)
-                    W[j] = philox_block(bb[b] | ((uint32_t)j << 20), c1, g0, g1, k0, k1);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int k = 4 * b + q, x = base + rel(k, lane);
                     act[k] = x >= x0 && x < xend;
                     int e[kSeqFirstWords];
 #pragma unroll
-                    for (int j = 0; j < kSeqFirstWords; ++j) e[j] = try_word(pick4(W[j], q));
+                    for (int j = 0; j < kSeqFirstWords; ++j) e[j] = try_word(pick4(Wn[b * kSeqFirstWords + j], q));
                     i[k] = e[kSeqFirstWords - 1];
 #pragma unroll
                     for (int j = kSeqFirstWords - 2; j >= 0; --j) i[k] = e[j] >= 0 ? e[j] : i[k];
@@ -400,7 +427,7 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
                     SEQ_STAT(st, st->v[kStLaneIters]++);
 #pragma unroll
                     for (int b = 0; b < NB; ++b) {
-                        const uint4 W = philox_block(bb[b] | (j0 << 20), c1, g0, g1, k0, k1);
+                        const uint4 W = philox_block(bb[b] | (j0 << 20), c1, g0, g1, LDPC_SEQ_KEYS);
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
                             const int k = 4 * b + q;
@@ -434,7 +461,7 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
                 const int own = ent & 63, kk = ent >> 6;
                 const uint32_t jj = j0 + (uint32_t)kl;
                 const uint32_t ob = (uint32_t)(base >> 2) + (uint32_t)(own + 64 * (kk >> 2));
-                const uint4 W = philox_block(ob | (jj << 20), c1, g0, g1, k0, k1);
+                const uint4 W = philox_block(ob | (jj << 20), c1, g0, g1, LDPC_SEQ_KEYS);
                 const int eh = (p < C && jj < 1024u) ? try_word(pick4(W, kk & 3)) : -1;
                 const uint64_t okm = __ballot(eh >= 0);
 #pragma unroll
@@ -462,10 +489,17 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
                 }
             }
             bool anyd = false;
+            uint32_t old[NS];
+#pragma unroll
+            for (int k = 0; k < NS; ++k) old[k] = act[k] ? atomicOr(&bm[i[k] >> 5], 1u << (i[k] & 31)) : 0u;
+            if (LDPC_SEQ_LOOKAHEAD) {  // the next round's first words in the atomics' latency
+                __builtin_amdgcn_sched_barrier(0);
+                first_words(base + 256 * NB);
+                __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
-                const uint32_t bit = 1u << (i[k] & 31);
-                dup[k] = act[k] && (atomicOr(&bm[i[k] >> 5], bit) & bit) != 0u;
+                dup[k] = act[k] && (old[k] & (1u << (i[k] & 31))) != 0u;
                 anyd |= dup[k];
             }
             int t = min(256 * NB, xend - base);  // kept: slots base + [x0 - base, t)
@@ -522,7 +556,7 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
                 else
                     *reinterpret_cast<int4 *>(ring + p) = make_int4(nv[0], nv[1], nv[2], nv[3]);
             }
-            if constexpr (EMIT) {
+            if (EMIT && out) {
 #pragma unroll
                 for (int k = 0; k < NS; ++k) {
                     const int s = rel(k, lane);
@@ -612,12 +646,13 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
     wave_sync();
     if (lane < R) {
         const int x = x0 + lane;
-        if constexpr (EMIT) out[x] = fin[lane];
+        if (EMIT && out) out[x] = fin[lane];
         ring[x & (kSeqRing - 1)] = (RT)fin[lane];
     }
     wave_sync();
     return validate(E);
 }
+#undef LDPC_SEQ_KEYS
 
 // Emit pass (and the whole sampler when start == nullptr): one wave per graph draws attempts
 // start[g], start[g] + 1, ... in order until one is simple (start[g] = the first simple attempt
@@ -883,8 +918,10 @@ __global__ __launch_bounds__(kWave) void sample_search_kernel(SampleShape sh, ui
         // draw into it (a simple one is then the graph itself unless a helper's lower attempt wins
         // -- the emit pass redraws exactly those graphs); helpers only search
         const bool solo = !helping;
-        const bool ok = solo ? seq_attempt<CSR, true, RT>(c, att, scratch_a + (size_t)g * sh.E, pools, &best[g], stp)
-                             : seq_attempt<CSR, false, RT>(c, att, nullptr, pools, &best[g], stp);
+        // one instantiation for both roles (out == nullptr: search only): half the code, and a
+        // simpler control-flow graph for the round loop
+        const bool ok = seq_attempt<CSR, true, RT>(c, att, solo ? scratch_a + (size_t)g * sh.E : nullptr, pools,
+                                                   &best[g], stp);
         SEQ_STAT(stp, stp->lap(kStCycRingVal); stp->v[kStAttempts]++;
                  stp->v[kStCycAttempt] += __builtin_amdgcn_s_memtime() - t_att; stp->flush());
         if (ok && lane == 0) {

@@ -50,15 +50,36 @@ def _free_port():
         return sk.getsockname()[1]
 
 
-def spawn_ranks(envs, argv, script=None):
+class _Stop(Exception):
+    def __init__(self, signum):
+        super().__init__(signum)
+        self.signum = signum
+
+
+def spawn_ranks(envs, argv, script=None, grace=5.0):
     """Start one child process per rank (never exec: this process has not touched the GPU,
     and stays the parent); rank 0's stdout (the JSON line) passes through.  Returns the
-    worst exit code; if a rank fails the others are terminated."""
+    worst exit code; if a rank fails the others are terminated.  SIGTERM / SIGHUP / SIGINT
+    aimed at this process alone (a scheduler or watchdog that signals only the parent) are
+    forwarded: the ranks get SIGTERM, then SIGKILL after `grace` seconds, and the parent
+    returns 128 + signum -- no rank is left holding a GPU or writing checkpoints."""
+    import signal
     import subprocess
     script = script or os.path.abspath(sys.argv[0])
-    procs = [subprocess.Popen([sys.executable, "-u", script] + list(argv), env=e) for e in envs]
+
+    def _raise(signum, _frame):
+        raise _Stop(signum)
+
+    saved = {}
+    for sig in (signal.SIGTERM, signal.SIGHUP, signal.SIGINT):
+        try:
+            saved[sig] = signal.signal(sig, _raise)
+        except ValueError:  # not the main thread: no handlers (the finally block still reaps)
+            pass
+    procs = []
     rc = 0
     try:
+        procs = [subprocess.Popen([sys.executable, "-u", script] + list(argv), env=e) for e in envs]
         while procs:
             for p in list(procs):
                 c = p.poll()
@@ -70,7 +91,19 @@ def spawn_ranks(envs, argv, script=None):
                     for q in procs:  # a failed rank: the others would wait in a collective forever
                         q.terminate()
             time.sleep(0.05)
+    except _Stop as st:
+        rc = 128 + st.signum
     finally:
+        for sig, h in saved.items():
+            signal.signal(sig, h)
         for p in procs:
-            p.kill()
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.time() + grace
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.0, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
     return rc

@@ -277,10 +277,18 @@ def ref_ml_system(parity_check, word, n, dv, dc):
     return target.astype(np.uint8), rem[: ne * (n - k)].astype(np.uint8).reshape(ne, n - k)
 
 
+def ref_srand(seed):
+    """Seed glibc's rand() -- the stream the reference generator draws from (it seeds only on
+    first_run, random_code_generator.c:22-25) -- so reference samples do not depend on how many
+    rand() calls earlier code in the process made."""
+    ct.CDLL(None).srand(ct.c_uint(seed))
+
+
 def ref_generate_random_code(n, dv, dc):
     """Drive _ref/random_code_generator.so with the 10-argument call of
     parallel_simulator_expurgated.py:201-223 (first_run=False: glibc rand() stream,
-    deterministic per process).  Returns (check_lookup, variable_lookup, H)."""
+    deterministic per process once ref_srand has seeded it).  Returns (check_lookup,
+    variable_lookup, H)."""
     k = int(n * (dc - dv) / dc)
     lib_ = ct.CDLL(os.path.join(REF_DIR, "random_code_generator.so"))
     check_lookup = np.zeros(n * dv, dtype="int32")

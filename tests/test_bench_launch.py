@@ -80,3 +80,36 @@ def test_bench_refuses_gpus_beyond_visible_without_gpu():
                        text=True, timeout=300, env={k: v for k, v in os.environ.items() if k != "WORLD_SIZE"})
     assert p.returncode == 2 and p.stdout.strip() == ""
     assert "--gpus 8" in p.stderr
+
+
+def test_spawn_ranks_forwards_sigterm_to_children(tmp_path):
+    """A SIGTERM aimed at the parent PID alone (a scheduler or watchdog) ends every rank: the
+    parent forwards it (SIGTERM, then SIGKILL after the grace period) and exits 128 + 15."""
+    import signal
+    import time
+    stub = tmp_path / "sleeper.py"
+    stub.write_text("import os, sys, time\n"
+                    "open(os.path.join(sys.argv[1], 'pid%s' % os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+                    "time.sleep(120)\n")
+    parent = tmp_path / "parent.py"
+    parent.write_text("import os, sys\n"
+                      f"sys.path.insert(0, {ROOT!r})\n"
+                      "from iib_project_ldpc_codes_amd.launch import launch_plan, spawn_ranks\n"
+                      "mode, envs = launch_plan(3, dict(os.environ), 8)\n"
+                      f"sys.exit(spawn_ranks(envs, [{str(tmp_path)!r}], script={str(stub)!r}, grace=2.0))\n")
+    env = {k: v for k, v in os.environ.items() if k != "WORLD_SIZE"}
+    p = subprocess.Popen([sys.executable, str(parent)], env=env)
+    deadline = time.time() + 60
+    while len(list(tmp_path.glob("pid*"))) < 3 and time.time() < deadline:
+        time.sleep(0.1)
+    pids = [int(f.read_text()) for f in tmp_path.glob("pid*")]
+    assert len(pids) == 3
+    os.kill(p.pid, signal.SIGTERM)
+    assert p.wait(timeout=30) == 128 + signal.SIGTERM
+    for pid in pids:
+        try:
+            os.kill(pid, 0)
+            alive = True
+        except ProcessLookupError:
+            alive = False
+        assert not alive, f"rank pid {pid} survived the parent's SIGTERM"

@@ -8,7 +8,8 @@ unchanged into oracle/_ref):
   goodness of fit to uniform -- the law is a uniform socket permutation conditioned on
   simple checks, so every slot's variable is uniform over the n variables.
 
-Seeds are fixed, so the tests are deterministic; the thresholds are p >= 1e-3."""
+Seeds are fixed (the reference's glibc rand() stream is seeded with oracle.ref_srand before its
+samples are drawn), so the tests are deterministic and independent of test order; the thresholds are p >= 1e-3."""
 import numpy as np
 import pytest
 from scipy import stats
@@ -65,6 +66,7 @@ def test_one_level_sampler_law_full_distribution():
     if not oracle.ref_available():
         pytest.skip("oracle/_ref not built")
     n, N = 40, 2000
+    oracle.ref_srand(7)  # the reference draws from glibc rand(): seed it, so the test does not depend on test order
     ref = [oracle.ref_generate_random_code(n, 3, 6)[0] for _ in range(N)]
     _check_c4_and_slots(n, _ours(n, N, 101), ref)
 
@@ -73,5 +75,6 @@ def test_one_level_sampler_law_full_distribution():
 def test_seq_sampler_law_full_distribution(force_seq, n, N):
     if not oracle.ref_available():
         pytest.skip("oracle/_ref not built")
+    oracle.ref_srand(11 + n)
     ref = [oracle.ref_generate_random_code(n, 3, 6)[0] for _ in range(N)]
     _check_c4_and_slots(n, _ours(n, N, 202), ref)
