@@ -13,7 +13,7 @@ Weak scaling: every rank decodes its own 65536-frame batch.
 Rank 0 prints one JSON line.  roofline: the decode kernel keeps every edge
 message in LDS, so its binding unit is on-chip: LDS cycles (per CU) or VALU
 issue cycles (per SIMD) per codeword-iteration from the committed HEAD issue
-model (profiles/r02e_issue_model.json, scripts/issue_model.py) x the live
+model (ISSUE_PROFILE below, scripts/issue_model.py) x the live
 codeword-iteration rate of the kernel (HIP events on the launch stream) over
 the unit's peak; the larger fraction is `roofline`.  roofline.hbm_model
 keeps SURVEY.md 8(d)'s streaming byte model (2*E*4 + 2*n*4 = 320,000 B per
@@ -175,19 +175,23 @@ def graph_cfg0():
     return TannerGraph.random_regular(1000, DV, DC, seed=1)
 
 
-ISSUE_PROFILE = os.path.join(ROOT, "profiles", "r04b_issue_model.json")
+ISSUE_PROFILE = os.path.join(ROOT, "profiles", "r05a_issue_model.json")
 SIMDS, CUS, CLOCK_HZ = 1024, 256, 2.4e9
 
 
 def onchip_rooflines(cw_iters_per_s, kernel):
-    """The units the LDS-resident kernel can saturate, from the committed HEAD issue model
-    (profiles/r02e_issue_model.json, scripts/issue_model.py: the kernel ISA's blocks x their
+    """The units the LDS-resident kernel can saturate, per codeword-iteration, from the committed
+    HEAD issue model (ISSUE_PROFILE, scripts/issue_model.py: the kernel ISA's blocks x their
     execution counts, cross-checked with and completed by the PMC counters of one launch):
-      valu: issue cycles per codeword-iteration (packed f32 4, plain 2, transcendental 8 per
-            wave64 instruction, MI355X_MICROARCH.md) over 1024 SIMDs x 2.4 GHz;
-      lds:  LDS cycles per codeword-iteration -- the conflict-free per-instruction costs of the
-            MI355X_MICROARCH.md LDS table PLUS the measured SQ_LDS_BANK_CONFLICT cycles (the pipe
-            is busy for both) -- over 256 CUs x 2.4 GHz; the conflict-free fraction beside it.
+      valu: issue cycles per codeword-iteration at the MEASURED wave64 prices (plain f32 / integer
+            4.2, packed f32 5.3, transcendental 8.2; scripts/diag/valu_rate.hip,
+            profiles/r05_valu_rate*.jsonl) over 1024 SIMDs x 2.4 GHz; beside it the PMC
+            VALU-active fraction of the profiled launch (SQ_ACTIVE_INST_VALU counts 4 / 4 / 8);
+      lds:  LDS-array cycles per codeword-iteration MEASURED by SQ_LDS_IDX_ACTIVE (every array
+            cycle, bank conflicts included) over 256 CUs x 2.4 GHz; beside it the older transfer
+            model (MI355X_MICROARCH.md per-instruction costs -- a store's address + data transfer,
+            not its array cycles -- plus SQ_LDS_BANK_CONFLICT, which double-counts store conflicts
+            that hide under the transfer).
     achieved = cycles x the live codeword-iteration rate of the kernel.  Returns (valu, lds), or
     (None, None) when the committed model is of another kernel than the one that ran."""
     if not os.path.exists(ISSUE_PROFILE):
@@ -198,42 +202,41 @@ def onchip_rooflines(cw_iters_per_s, kernel):
         return None, None
     rel = os.path.relpath(ISSUE_PROFILE, ROOT)
     v_cyc = d["valu_issue_cycles_per_codeword_iteration"]
-    l_cyc = d["lds_cycles_per_codeword_iteration"]
     valu = {"bound": "valu", "achieved": v_cyc * cw_iters_per_s / 1e9, "peak": SIMDS * CLOCK_HZ / 1e9,
             "unit": "G SIMD-issue-cycles/s", "frac": v_cyc * cw_iters_per_s / (SIMDS * CLOCK_HZ),
             "issue_cycles_per_codeword_iteration": v_cyc,
             "wave_instr_per_codeword_iteration": d["wave_instr_per_codeword_iteration"],
-            "cycles_per_wave_instr": d["cycles"]["valu"], "profile": rel, "profile_git": d.get("git")}
-    alg = algorithmic_valu_cycles()
+            "cycles_per_wave_instr": d["cycles"]["valu"], "prices": d.get("valu_prices"),
+            "profile": rel, "profile_git": d.get("git")}
+    alg = algorithmic_valu_cycles(d["cycles"]["valu"])
     valu["algorithmic"] = {"issue_cycles_per_codeword_iteration": alg["cycles"],
                            "frac": alg["cycles"] * cw_iters_per_s / (SIMDS * CLOCK_HZ), "definition": alg["definition"]}
     pmc = d.get("pmc_per_codeword_iteration", {})
-    prof_pmc = os.path.join(ROOT, "profiles", d.get("pmc_summary") or
-                            os.path.basename(ISSUE_PROFILE).replace("_issue_model.json", "_pmc_summary.json"))
-    if os.path.isfile(prof_pmc):  # VALU-active fraction of the profiled launch (PMC, not the model)
-        with open(prof_pmc) as f:
-            c = json.load(f)["counters"]
-        kernel_cycles = c["GRBM_GUI_ACTIVE"] / 8  # per XCD = the dispatch's shader-clock cycles
-        valu["pmc_valu_active_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / kernel_cycles
-        valu["pmc_profile"] = os.path.relpath(prof_pmc, ROOT)
-    elif pmc:
-        valu["pmc_valu_active_frac"] = None
+    if "SQ_ACTIVE_INST_VALU" in pmc:  # VALU-active cycles per codeword-iteration (PMC, quad-cycles x 4)
+        valu["pmc_valu_active_frac"] = pmc["SQ_ACTIVE_INST_VALU"] * 4 * cw_iters_per_s / (SIMDS * CLOCK_HZ)
+    t_cyc = d["lds_cycles_per_codeword_iteration"]
     conf = d["lds_bank_conflict_cycles_per_codeword_iteration"]
-    lds = {"bound": "lds", "achieved": (l_cyc + conf) * cw_iters_per_s / 1e9, "peak": CUS * CLOCK_HZ / 1e9,
-           "unit": "G LDS-cycles/s", "frac": (l_cyc + conf) * cw_iters_per_s / (CUS * CLOCK_HZ),
-           "conflict_free_frac": l_cyc * cw_iters_per_s / (CUS * CLOCK_HZ),
-           "lds_cycles_per_codeword_iteration": l_cyc + conf,
-           "conflict_free_lds_cycles_per_codeword_iteration": l_cyc,
-           "lds_instr_per_codeword_iteration": d["lds_instr_per_codeword_iteration"],
-           "bank_conflict_cycles_per_codeword_iteration": d["lds_bank_conflict_cycles_per_codeword_iteration"],
-           "cycles_per_wave_instr": d["cycles"]["lds"], "profile": rel, "profile_git": d.get("git")}
+    model = {"frac": (t_cyc + conf) * cw_iters_per_s / (CUS * CLOCK_HZ),
+             "cycles_per_codeword_iteration": t_cyc + conf, "conflict_free_cycles": t_cyc,
+             "bank_conflict_cycles": conf, "cycles_per_wave_instr": d["cycles"]["lds"],
+             "lds_instr_per_codeword_iteration": d["lds_instr_per_codeword_iteration"]}
+    idx = pmc.get("SQ_LDS_IDX_ACTIVE")
+    if idx:
+        lds = {"bound": "lds", "achieved": idx * cw_iters_per_s / 1e9, "peak": CUS * CLOCK_HZ / 1e9,
+               "unit": "G LDS-array-cycles/s", "frac": idx * cw_iters_per_s / (CUS * CLOCK_HZ),
+               "array_cycles_per_codeword_iteration": idx, "source": "PMC SQ_LDS_IDX_ACTIVE (measured)",
+               "transfer_model": model, "profile": rel, "profile_git": d.get("git")}
+    else:  # an older profile without the array counter: the model
+        lds = {"bound": "lds", "achieved": (t_cyc + conf) * cw_iters_per_s / 1e9, "peak": CUS * CLOCK_HZ / 1e9,
+               "unit": "G LDS-cycles/s", "frac": model["frac"], "source": "transfer model + SQ_LDS_BANK_CONFLICT",
+               "transfer_model": model, "profile": rel, "profile_git": d.get("git")}
     return valu, lds
 
 
-def algorithmic_valu_cycles():
+def algorithmic_valu_cycles(prices=None):
     """The minimum VALU issue work of the headline decode per codeword-iteration in its chosen
     formulation (no unpacks, clamps, sign handling, staging or loop control), SIMD-cycles at the
-    issue-model prices (packed f32 4, transcendental 8 per wave64 instruction):
+    issue-model prices (packed f32 and transcendental, per wave64 instruction):
       check phase, per check pair (both degree-6 checks on float2, elementary-symmetric rule):
         prefix (E, O) 4 x 2 packed ops, suffix 3 x (2 v_pk_mul + 4 v_pk_fma) + 4 for the last step
         (its prefix set is {R_0}: no product), six output ratios 6 v_pk_mul + 12 v_rcp_f32
@@ -241,16 +244,17 @@ def algorithmic_valu_cycles():
       variable phase, per variable pair (degree 3: one local + two gathered ratios on float2):
         R_j = E prod_{k != j} r_k by prefix / suffix products = 5 v_pk_mul.
     For (3,6) n = 10,000: P = 2,500 check pairs, 5,000 variable pairs, 64 lanes per wave."""
+    pk, tr = (prices or {}).get("packed", 4.0), (prices or {}).get("trans", 8.0)
     P, VPAIRS = (N_BITS // 2) // 2, N_BITS // 2
-    check = (36 * 4 + 12 * 8) * P / 64
-    var = 5 * 4 * VPAIRS / 64
+    check = (36 * pk + 12 * tr) * P / 64
+    var = 5 * pk * VPAIRS / 64
     return {"cycles": check + var,
-            "definition": "check pair: 36 v_pk_* x4 + 12 v_rcp x8 cycles per 64 pairs; variable pair: 5 v_pk_mul x4 "
-                          "per 64 pairs; P=2500, 5000 variable pairs (bench.py algorithmic_valu_cycles)"}
+            "definition": f"check pair: 36 v_pk_* x{pk:g} + 12 v_rcp x{tr:g} cycles per 64 pairs; variable pair: "
+                          f"5 v_pk_mul x{pk:g} per 64 pairs; P=2500, 5000 variable pairs (bench.py algorithmic_valu_cycles)"}
 
 
 def load_traffic():
-    for name in ("r04b_pmc_traffic.json", "r03a_pmc_traffic.json", "pmc_traffic.json"):
+    for name in ("r05a_pmc_traffic.json", "r04b_pmc_traffic.json", "r03a_pmc_traffic.json", "pmc_traffic.json"):
         p = os.path.join(ROOT, "profiles", name)
         if os.path.exists(p):
             with open(p) as f:

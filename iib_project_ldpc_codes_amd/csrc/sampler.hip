@@ -146,9 +146,6 @@ constexpr int kSeqFirstWords = LDPC_SEQ_FIRST_WORDS;
 #define LDPC_SEQ_WIDE_R 0  // > 0: pools of at least this many entries draw 512 slots per round
 #endif                     // (measured slower at n = 64,800: more registers, costlier collisions)
 constexpr int kSeqWideR = LDPC_SEQ_WIDE_R;
-#ifndef LDPC_SEQ_LOOKAHEAD
-#define LDPC_SEQ_LOOKAHEAD 0  // 1: each round computes the next round's first-word Philox blocks (see rounds;
-#endif                        // measured 2 % slower at n = 64,800: the search pass is issue-bound)
 #ifndef LDPC_SEQ_VKEYS
 #define LDPC_SEQ_VKEYS 1  // the attempt's Philox key schedule in VGPRs (PhiloxKeys)
 #endif
@@ -342,13 +339,10 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
         };
         auto rel = [&](int k, int l) { return 256 * (k >> 2) + 4 * l + (k & 3); };  // slot k of lane l
         // The first words of every slot of the round at base bs: the NB x kSeqFirstWords Philox
-        // blocks of the lane, computed round-interleaved.  Each round computes the NEXT round's
-        // blocks (for base + 256 NB, right after its bitmap atomics are issued, so the ten-step
-        // product chains run in the atomics' / ring's LDS latency); a round whose base differs
-        // (a collision kept fewer slots) recomputes its own.  Words depend only on (slot, j), so
-        // the schedule changes no result.
+        // blocks of the lane, computed round-interleaved (philox_blocks: their ten-step product
+        // chains overlap).  (Computing the next round's blocks in this round's atomics' latency
+        // measured slower: the search pass is issue-bound; scripts/ablations/README.md.)
         uint4 Wn[NB * kSeqFirstWords];
-        int pbase = -1;
         auto first_words = [&](int bs) {
             uint32_t cc[NB * kSeqFirstWords];
 #pragma unroll
@@ -357,7 +351,6 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
                 for (int j = 0; j < kSeqFirstWords; ++j)
                     cc[b * kSeqFirstWords + j] = ((uint32_t)(bs >> 2) + (uint32_t)(lane + 64 * b)) | ((uint32_t)j << 20);
             philox_blocks<NB * kSeqFirstWords>(cc, c1, g0, g1, LDPC_SEQ_KEYS, Wn);
-            pbase = bs;
         };
         while (x0 < xend) {
             if (best && (++nround & 15) == 0) {  // search: a lower simple attempt makes this one moot
@@ -383,7 +376,7 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
             uint32_t bb[NB];
 #pragma unroll
             for (int b = 0; b < NB; ++b) bb[b] = (uint32_t)(base >> 2) + (uint32_t)(lane + 64 * b);
-            if (base != pbase) first_words(base);  // the last round's look-ahead guessed another base
+            first_words(base);
             int i[NS];
             bool act[NS], need[NS];
 #pragma unroll
@@ -489,17 +482,10 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
                 }
             }
             bool anyd = false;
-            uint32_t old[NS];
-#pragma unroll
-            for (int k = 0; k < NS; ++k) old[k] = act[k] ? atomicOr(&bm[i[k] >> 5], 1u << (i[k] & 31)) : 0u;
-            if (LDPC_SEQ_LOOKAHEAD) {  // the next round's first words in the atomics' latency
-                __builtin_amdgcn_sched_barrier(0);
-                first_words(base + 256 * NB);
-                __builtin_amdgcn_sched_barrier(0);
-            }
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
-                dup[k] = act[k] && (old[k] & (1u << (i[k] & 31))) != 0u;
+                const uint32_t bit = 1u << (i[k] & 31);
+                dup[k] = act[k] && (atomicOr(&bm[i[k] >> 5], bit) & bit) != 0u;
                 anyd |= dup[k];
             }
             int t = min(256 * NB, xend - base);  // kept: slots base + [x0 - base, t)

@@ -23,8 +23,13 @@
 template <int OP>
 __global__ __launch_bounds__(256) void kern(uint32_t *out, uint64_t *stamp, uint32_t seed, int reps) {
     uint32_t x[CHAINS];
+    uint64_t p[CHAINS], q[CHAINS];
 #pragma unroll
-    for (int i = 0; i < CHAINS; ++i) x[i] = seed * (threadIdx.x + 17 * i) + i;
+    for (int i = 0; i < CHAINS; ++i) {
+        x[i] = seed * (threadIdx.x + 17 * i) + i;
+        p[i] = (uint64_t)x[i] * 0x9E3779B97F4A7C15ull;
+        q[i] = 0x3F8000013F800001ull ^ ((uint64_t)i << 3);
+    }
     const uint32_t K = 0x3F800001u ^ seed;
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int r = 0; r < reps; ++r) {
@@ -43,13 +48,22 @@ __global__ __launch_bounds__(256) void kern(uint32_t *out, uint64_t *stamp, uint
                 if constexpr (OP == 4) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(x[i]) : "s"(K));
                 if constexpr (OP == 5) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[i]) : "s"(K));
                 if constexpr (OP == 6) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x[i]) : "v"(K));
+                // packed f32 with distinct operand pairs (OP 2 reads one pair three times)
+                if constexpr (OP == 7) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(p[i]) : "v"(q[i]));
+                if constexpr (OP == 8) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(p[i]) : "v"(q[i]), "v"(q[(i + 1) % CHAINS]));
+                if constexpr (OP == 9) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(p[i]) : "v"(q[i]));
+                if constexpr (OP == 10) {  // one packed FMA + one plain add, independent
+                    asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(p[i]) : "v"(q[i]), "v"(q[(i + 1) % CHAINS]));
+                    asm volatile("v_add_f32 %0, %1, %0" : "+v"(x[i]) : "s"(K));
+                }
+                if constexpr (OP == 11) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(p[i]) : "v"(x[i]), "s"(K) : "vcc");
             }
         }
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     uint32_t a = 0;
 #pragma unroll
-    for (int i = 0; i < CHAINS; ++i) a ^= x[i];
+    for (int i = 0; i < CHAINS; ++i) a ^= x[i] ^ (uint32_t)p[i] ^ (uint32_t)(p[i] >> 32);
     out[blockIdx.x * blockDim.x + threadIdx.x] = a;
     if (threadIdx.x == 0) {
         stamp[2 * blockIdx.x] = t1 - t0;
@@ -124,5 +138,10 @@ int main() {
     sweep<4>("v_xor_b32");
     sweep<5>("v_mul_lo_u32");
     sweep<6>("v_cndmask_b32");
+    sweep<7>("v_pk_mul_f32 distinct");
+    sweep<8>("v_pk_fma_f32 distinct");
+    sweep<9>("v_pk_add_f32 distinct");
+    sweep<10>("v_pk_fma_f32 + v_add_f32 (2 instr)");
+    sweep<11>("v_mad_u64_u32");
     return 0;
 }

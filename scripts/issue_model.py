@@ -8,8 +8,7 @@ usage: python scripts/issue_model.py <kernels.s> <pmc_summary.json> <out.json> [
 The two on-chip units an LDS-resident decode kernel can saturate, per codeword-iteration:
 
 * VALU issue (per SIMD): wave-instructions by class x issue cycles of one wave64 instruction
-  on its SIMD (MI355X_MICROARCH.md: v_fma_f32 2 cycles on the SIMD-32, packed f32 twice that,
-  transcendentals 8).  packed = the ISA's v_pk_* of every block x its wave-executions;
+  on its SIMD (measured, VALU_CYC below: plain 4.2, packed f32 5.3, transcendentals 8.2).  packed = the ISA's v_pk_* of every block x its wave-executions;
   trans = PMC SQ_INSTS_VALU_TRANS_F32; plain = PMC SQ_INSTS_VALU - packed - trans.
   Peak: 1024 SIMDs.
 * LDS (per CU): the blocks' ds_* wave-instructions x their conflict-free LDS cycles
@@ -47,7 +46,15 @@ LDS_CYC = {"ds_read_b128": 4, "ds_write_b128": 13, "ds_read_b32": 2, "ds_write_b
            "ds_read2_b32": 4, "ds_read2st64_b32": 4, "ds_read2_b64": 4, "ds_write2_b64": 13,
            "ds_read_u8": 2, "ds_write_b8": 4, "ds_read_u16": 2, "ds_write_b16": 4, "ds_bpermute_b32": 2,
            "ds_swizzle_b32": 2, "ds_add_u32": 4, "ds_or_b32": 4, "ds_read_b96": 4, "ds_write_b96": 13}
-VALU_CYC = {"packed": 4.0, "plain": 2.0, "trans": 8.0}
+# Issue cycles of one wave64 VALU instruction on its SIMD, measured on the whole chip by
+# scripts/diag/valu_rate.hip (HIP events around 5 launches of 256 x W workgroups, W = 8 waves per
+# SIMD, throughput at the in-kernel clock; profiles/r05_valu_rate*.jsonl): v_add / v_fma / v_xor /
+# v_mul_lo 4.1-4.3 (4.2), v_pk_mul / v_pk_fma / v_pk_add with distinct operand pairs 5.2-5.3 (5.3),
+# v_rcp_f32 8.2 -- not the 2 / 4 / 8 of rounds 2-4 (MI355X_MICROARCH.md's SIMD-32 figure for a
+# wave64 v_fma_f32).  PMC SQ_ACTIVE_INST_VALU counts one quad-cycle per plain or packed
+# instruction and two per transcendental (4 / 4 / 8: the headline launch's count to 0.1 %), so
+# it undercounts the packed ops' measured cost; both are reported.
+VALU_CYC = {"packed": 5.3, "plain": 4.2, "trans": 8.2}
 KERNELS = {
     "loc": ("_ZN4ldpc12_GLOBAL__N_113bp_loc_kernelILi6ELi6ELi2ELi2ELi5ELi512ELi0ELb0ELb0ELb0ELb0ELb0EEEvNS0_6BpArgsE",
             "bp_loc_kernel<6,6,2,2,KP=5,T=512,SPA,fixed-count>", 512, 5),
@@ -78,8 +85,13 @@ def loc_parts(bb, T, KP, stats=None):
         r_chk, r_var, r_cw = 1.0, (ITERS - 1) / ITERS, 1.0 / ITERS
     # check slot k: the block storing the pair's two ds_write_b128 (the early-stop builds load
     # one of the two b128 inputs as a b128 and the other through two narrower reads)
+    # (round 5: the one-class check phase has no per-pair branch -- one block holding all KP
+    # pairs' 2 * KP ds_write_b128, run by every wave)
     chk = [i for i, (_, ins) in enumerate(bb) if ins.count("ds_write_b128") == 2]
-    assert len(chk) == KP, len(chk)
+    one = [i for i, (_, ins) in enumerate(bb) if ins.count("ds_write_b128") == 2 * KP]
+    if len(one) == 1 and len(chk) != KP:
+        chk = one
+    assert len(chk) in (KP, 1), len(chk)
     # variable phase: the blocks after the check slots holding its 8*KP ds_read_b32 / ds_write_b32
     # (one block; split in ten by the slab-store branches in the early-stop-with-posteriors build)
     # (searched from the last check slot on, wrapping: the compiler may rotate the loop so the
@@ -95,7 +107,7 @@ def loc_parts(bb, T, KP, stats=None):
     assert nr == 8 * KP and sum(bb[i][1].count("ds_write_b32") for i in var) == 8 * KP, (var, nr)
     execs = {}
     for k, i in enumerate(chk):
-        lanes = min(max(P - k * T, 0), T)
+        lanes = min(max(P - k * T, 0), T) if len(chk) == KP else T
         execs[i] = (lanes + 63) // 64 * r_chk
     for i in var:
         execs[i] = waves * r_var

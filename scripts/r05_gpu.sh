@@ -37,7 +37,13 @@ for step in "$@"; do
       timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.log 2>&1 || { tail -20 gpurun_out/bench_$TAG.log; exit 1; }
       tail -1 gpurun_out/bench_$TAG.log ;;
     prof)
-      TAG=$TAG KREGEX=bp_loc ./scripts/profile.sh > gpurun_out/profile_$TAG.log 2>&1 || { tail -20 gpurun_out/profile_$TAG.log; exit 1; }
+      PMC_GROUPS="FETCH_SIZE
+WRITE_SIZE
+SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS
+SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT
+SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_SALU
+SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_BRANCH" \
+        TAG=$TAG KREGEX=bp_loc ./scripts/profile.sh > gpurun_out/profile_$TAG.log 2>&1 || { tail -20 gpurun_out/profile_$TAG.log; exit 1; }
       tail -30 gpurun_out/profile_$TAG.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
