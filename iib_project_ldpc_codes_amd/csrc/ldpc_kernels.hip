@@ -32,32 +32,14 @@ namespace {
 #ifndef LDPC_LDS36_PREFETCH
 #define LDPC_LDS36_PREFETCH 1  // persistent LDS kernel (decode API) prefetching the next codeword's LLRs
 #endif
-#ifndef LDPC_SPA_PROD
-#define LDPC_SPA_PROD 1  // bp_lds_kernel sum-product without early stop: product-domain variable phase
-#endif
-#ifndef LDPC_MS_LAUNDER
-#define LDPC_MS_LAUNDER 1  // min-sum: scaled minima computed once per check (see check_update_ms6)
-#endif
-#ifndef LDPC_ET_DELTA
-#define LDPC_ET_DELTA 1  // early stop: rewrite a variable's hard-decision bytes only when it changes
-#endif
 #ifndef LDPC_BEC_DEC_BITS
 #define LDPC_BEC_DEC_BITS 1  // batch BEC decode (B >= 64) on the bit-sliced kernel when its planes fit LDS
-#endif
-#ifndef LDPC_SPA_RWIRE
-#define LDPC_SPA_RWIRE 1  // bp_lds_kernel sum-product: v->c wire = the clamped ratio R itself (see ratio_wire)
 #endif
 #ifndef LDPC_LOC_VGROUP
 #define LDPC_LOC_VGROUP 1  // bp_loc_kernel: variable pairs per scheduling group (0: no barriers)
 #endif
-#ifndef LDPC_LOC_LAUNDER_SP
-#define LDPC_LOC_LAUNDER_SP 1  // bp_loc_kernel: no loop-invariant unpacked gather addresses
-#endif
 #ifndef LDPC_LOC_CGROUP
 #define LDPC_LOC_CGROUP 1  // bp_loc_kernel: check pairs per scheduling group (0: no barriers)
-#endif
-#ifndef LDPC_CHECK_W64
-#define LDPC_CHECK_W64 0  // check phase writes each pair edge with its own ds_write_b64
 #endif
 // ===========================================================================
 // 1. BEC erasure decoding -- message_passing.c:7-82, bit-exact.
@@ -585,83 +567,49 @@ template <int ALGO> __device__ __forceinline__ float to_msg(float l) {
     else return l + 0.0f;
 }
 
-// Sum-product check rule in ratio form, shared by all kernels and restated by
-// oracle check_update_spa: for an input message x (log2 units here) e = 2^-min(|x|, 23),
-// a = sign(x) * (1 - e) and b = 2 - |a| (= 1 + e), so tanh(x/2) = a / b; the
-// exclusive products N_j = prod_{i != j} a_i, D_j = prod_{i != j} b_i give the
-// output 2 atanh(N_j / D_j) / ln 2 = log2((D_j + N_j) / (D_j - N_j)), with
-// D_j +- N_j formed as fma(prefix_b_j, suffix_b_j, +-N_j).
+// Sum-product check rule in ratio form, restated by oracle check_update_spa: for an
+// input message x (log2 units here) tanh(x/2) = (R - 1) / (R + 1) with the ratio
+// R = 2^x, |x| clamped to 23 (R in [2^-23, 2^23]); the exclusive products of the
+// (R - 1) and (R + 1) terms give the output 2 atanh(N_j / D_j) / ln 2 =
+// log2((D_j + N_j) / (D_j - N_j)) -- formed without cancellation from elementary
+// symmetric polynomials of the R (check_update_spa_pair_rwire).
 //
-// v->c message "on the wire" of the LDS kernel: sum-product sends a itself, so the
-// exponential runs in the variable phase and the check phase only forms
-// b = 2 - |a|; min-sum sends x itself.
-template <int ALGO>
-__device__ __forceinline__ float v2c_wire(float x) {
-    if (ALGO == 0) return copysignf(1.0f - __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x), 0.0f, 23.0f)), x);
-    return x;
-}
-// R-wire of the irregular kernel: the clamped ratio 2^x (check_update<0, D, true> input)
+// v->c message "on the wire" of the LDS kernels: sum-product sends the clamped ratio R
+// itself (the check rule's outputs (D + N) / (D - N) are invariant to a positive scale of
+// each input's (R - 1, R + 1) pair, so no reciprocal per edge in the variable phase;
+// magnitudes stay below 2^23 + 1, so the exclusive products of 5 inputs stay below
+// 2^116); min-sum sends x itself.
 template <int ALGO>
 __device__ __forceinline__ float v2c_rwire(float x) {
     if (ALGO == 0) return __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(x, -23.0f, 23.0f));
     return x;
 }
-template <int ALGO>
-__device__ __forceinline__ float2 v2c_wire2(float2 x) {
-    if (ALGO == 0) {
-        const float2 e = make_float2(__builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x.x), 0.0f, 23.0f)),
-                                     __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(x.y), 0.0f, 23.0f)));
-        const float2 a = make_float2(1.0f, 1.0f) - e;
-        return make_float2(copysignf(a.x, x.x), copysignf(a.y, x.y));
-    }
-    return x;
-}
-
-// Product domain (bp_lds_kernel PROD): for an extrinsic ratio R = 2^x the wire
-// value sign(x) (1 - 2^-min(|x|, 23)) of v2c_wire is
-//   min(R, 1) - min(1/R, 1)   (R >= 1: 1 - 1/R;  R < 1: R - 1)
-// with both terms clamped below at 2^-23 (|x| <= 23): two v_med3_f32, one
-// v_rcp_f32 in place of the v_exp_f32, one packed subtraction per two edges.
-// (The algebraically equal (Rc - 1) / max(Rc, 1) forms 1 - a ~ 1/R as a difference
-// of two numbers near 1 and loses it to rounding for large R.)
-//
-// LDPC_SPA_RWIRE: the wire carries R itself, clamped to [2^-23, 2^23] (|x| <= 23, as
-// above), and the check forms the pair (R - 1, R + 1) = (a, b) * (R + 1) / 2 instead of
-// (a, 2 - |a|): tanh(x/2) = (R - 1) / (R + 1), and the check rule's outputs
-// (D + N) / (D - N) are invariant to a positive scale of each input's (a, b).  No
-// reciprocal per edge in the variable phase; magnitudes stay below 2^23 + 1, so the
-// exclusive products of 5 inputs stay below 2^116.
-__device__ __forceinline__ float ratio_wire(float R) {
-    if (LDPC_SPA_RWIRE) return __builtin_amdgcn_fmed3f(R, 0x1p-23f, 0x1p23f);
-    return __builtin_amdgcn_fmed3f(R, 0x1p-23f, 1.0f) -
-           __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(R), 0x1p-23f, 1.0f);
-}
+// an extrinsic ratio R on the wire: clamped to [2^-23, 2^23]
+__device__ __forceinline__ float ratio_wire(float R) { return __builtin_amdgcn_fmed3f(R, 0x1p-23f, 0x1p23f); }
 __device__ __forceinline__ float2 ratio_wire2(float2 R) {
-    if (LDPC_SPA_RWIRE)
-        return make_float2(__builtin_amdgcn_fmed3f(R.x, 0x1p-23f, 0x1p23f), __builtin_amdgcn_fmed3f(R.y, 0x1p-23f, 0x1p23f));
-    const float2 lo = make_float2(__builtin_amdgcn_fmed3f(R.x, 0x1p-23f, 1.0f),
-                                  __builtin_amdgcn_fmed3f(R.y, 0x1p-23f, 1.0f));
-    const float2 u = make_float2(__builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(R.x), 0x1p-23f, 1.0f),
-                                 __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(R.y), 0x1p-23f, 1.0f));
-    return lo - u;
+    return make_float2(__builtin_amdgcn_fmed3f(R.x, 0x1p-23f, 0x1p23f), __builtin_amdgcn_fmed3f(R.y, 0x1p-23f, 0x1p23f));
 }
 
-#ifndef LDPC_MS_BITSIGN
-#define LDPC_MS_BITSIGN 1  // check_update_ms6: output signs by bit operations (see there)
-#endif
-// Inline-asm helpers (v_bitop3_b32, the VCC select, v_bfi_b32): the compiler's hazard
+// Inline-asm helpers (v_bitop3_b32, the VCC select): the compiler's hazard
 // recognizer does not look inside inline asm, so their operands must not be fresh
 // transcendental (v_exp / v_log / v_rcp) results -- every use below takes LDS loads, min /
 // med3 / mul / bfe results or values from an earlier phase.
 // v_bitop3_b32 (gfx950) with truth table T over (S0, S1, S2) = (0xF0, 0xCC, 0xAA)
+// (check_update_ms6's sign stamps stay in asm: through the builtin the fixed-count min-sum
+// decode measured 1.3 % slower, profiles/r05_ab_bitop3_builtin.txt)
 template <int T>
 __device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t r;
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "n"(T));
     return r;
 }
-// a ^ b ^ c in one instruction (gfx950 has no v_xor3_b32: v_bitop3_b32 with table 0x96)
-__device__ __forceinline__ uint32_t xor3u(uint32_t a, uint32_t b, uint32_t c) { return bitop3<0x96>(a, b, c); }
+// a ^ b ^ c in one instruction (gfx950 has no v_xor3_b32: v_bitop3_b32 with table 0x96).
+// Through the builtin, as bfi_u32: the hazard recognizer sees the instruction and inserts no
+// conservative s_nop around it (early stop +0.9 %, min-sum Monte-Carlo +1.2 %,
+// profiles/r05_ab_xor3_bfi_builtin.txt)
+__device__ __forceinline__ uint32_t xor3u(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 // |x| == m ? t : f as v_cmp (into VCC) + v_cndmask: the compiler would otherwise hold one
 // SGPR-pair mask per output of a check pair at once and spill SGPRs
 __device__ __forceinline__ uint32_t sel_abs_eq(float x, float m, uint32_t t, uint32_t f) {
@@ -669,18 +617,10 @@ __device__ __forceinline__ uint32_t sel_abs_eq(float x, float m, uint32_t t, uin
     asm("v_cmp_eq_f32_e64 vcc, |%1|, %2\n\tv_cndmask_b32 %0, %4, %3, vcc" : "=v"(r) : "v"(x), "v"(m), "v"(t), "v"(f) : "vcc");
     return r;
 }
-// (m & a) | (~m & b): one v_bfi_b32
+// (m & a) | (~m & b): one v_bitop3_b32 (table 0xCA), through the builtin (see xor3u)
 __device__ __forceinline__ uint32_t bfi_u32(uint32_t m, uint32_t a, uint32_t b) {
-    uint32_t o;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(o) : "v"(m), "v"(a), "v"(b));
-    return o;
+    return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);
 }
-#ifndef LDPC_LOC_POST_LOGE
-#define LDPC_LOC_POST_LOGE 1  // bp_loc_kernel SPA posteriors: channel term log2(E) from registers
-#endif
-#ifndef LDPC_LOC_MS_BFI
-#define LDPC_LOC_MS_BFI 1  // bp_loc_kernel min-sum: ordered variable sums by bfe/bfi selects (ms_sum)
-#endif
 // (r & ~1) | (d & 1): one v_bfi_b32
 // (plain C: the compiler emits one v_and_or_b32 / v_bfi_b32 and, unlike for inline asm, inserts
 // the wait state gfx950 needs when an operand is a fresh transcendental result -- an asm
@@ -749,18 +689,6 @@ __device__ __forceinline__ void check_update(float (&x)[D], float alpha, int d =
     }
 }
 
-// Sum-product update of a PAIR of checks held as float2 lanes (.x = check 2q,
-// .y = check 2q+1; bp_lds_kernel's interleaved layout): the same arithmetic as
-// check_update<0, D, true> per lane, with every product, sum and difference one
-// packed op for both checks.  a[] holds the wire values in and the outputs out.
-// 2 - |x| as one VOP3 op with an abs modifier (the vectoriser would otherwise
-// pack it as v_and + v_pk_add, 1.5 ops per value)
-[[maybe_unused]] __device__ __forceinline__ float two_minus_abs(float x) {
-    float r;
-    asm("v_sub_f32_e64 %0, 2.0, |%1|" : "=v"(r) : "v"(x));
-    return r;
-}
-
 // Normalized min-sum update of one degree-6 check, branch-free: the two smallest
 // magnitudes (with multiplicity) from two triples -- m1 = min of the triple minima,
 // m2 = min(max of the triple minima, both triple medians) -- via v_min3 / v_med3.
@@ -774,12 +702,9 @@ __device__ __forceinline__ void check_update_ms6(float (&x)[6], float alpha) {
     const float mn2 = fminf(fminf(ax[3], ax[4]), ax[5]), md2 = __builtin_amdgcn_fmed3f(ax[3], ax[4], ax[5]);
     const float m1 = fminf(mn1, mn2), m2 = fminf(fminf(fmaxf(mn1, mn2), md1), md2);
     float am1 = alpha * m1, am2 = alpha * m2;
-#if LDPC_MS_LAUNDER
     // keep the two products: otherwise select(alpha*m2, alpha*m1) is folded into
     // alpha*select(m2, m1), one multiply per edge instead of two per check
     asm volatile("" : "+v"(am1), "+v"(am2));
-#endif
-#if LDPC_MS_BITSIGN
     // signs as bits (no input is -0, see to_msg, so the sign bit is the oracle's x < 0):
     // S = XOR of the six sign bits, stamped onto both scaled minima once per check; each
     // output is then the selected minimum XOR its own input's sign bit -- v_cmp, v_cndmask
@@ -793,60 +718,11 @@ __device__ __forceinline__ void check_update_ms6(float (&x)[6], float alpha) {
         const uint32_t mag = sel_abs_eq(x[i], m1, s2, s1);  // a | (b & M), then a ^ (b & M)
         x[i] = __uint_as_float(bitop3<0x78>(mag, __float_as_uint(x[i]), M));
     }
-#else
-    bool neg = false;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) neg ^= (x[i] < 0.0f);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const float mag = ax[i] == m1 ? am2 : am1;
-        x[i] = (neg ^ (x[i] < 0.0f)) ? -mag : mag;
-    }
-#endif
 }
 
 
-// LOG = false (product-domain variable phase, bp_lds_kernel's PROD): the output
-// is the ratio (D+N)/(D-N) itself, i.e. 2^message; the log moves to the variable
-// phase's final posterior.
-template <int D, bool LOG = true>
-__device__ __forceinline__ void check_update_spa_pair(float2 (&a)[D]) {
-    float2 b[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) b[i] = make_float2(two_minus_abs(a[i].x), two_minus_abs(a[i].y));
-    // prefix products pn[i] = prod_{k<i} a_k (pd: of b), then one running suffix
-    // product walked down from the top: fewer live registers than two arrays
-    float2 pn[D], pd[D];
-    pn[1] = a[0];
-    pd[1] = b[0];
-#pragma unroll
-    for (int i = 2; i < D; ++i) {
-        pn[i] = pn[i - 1] * a[i - 1];
-        pd[i] = pd[i - 1] * b[i - 1];
-    }
-    // D_j +- N_j = pd_j * sd_j +- N_j as one fused multiply-add each (oracle: fmaf)
-    auto out = [](float2 N, float2 pdj, float2 sdj) {
-        const float2 P = pk_fma(pdj, sdj, N);
-        const float2 Q = pk_fma(pdj, sdj, make_float2(-N.x, -N.y));
-        const float2 r = P * make_float2(__builtin_amdgcn_rcpf(Q.x), __builtin_amdgcn_rcpf(Q.y));
-        if constexpr (!LOG) return r;
-        return make_float2(__builtin_amdgcn_logf(r.x), __builtin_amdgcn_logf(r.y));
-    };
-    const float2 one = make_float2(1.0f, 1.0f);
-    float2 sn = a[D - 1], sd = b[D - 1];
-    a[D - 1] = out(pn[D - 1], pd[D - 1], one);
-#pragma unroll
-    for (int i = D - 2; i >= 1; --i) {
-        const float2 N = pn[i] * sn;
-        const float2 r = out(N, pd[i], sd);
-        sn = sn * a[i];
-        sd = sd * b[i];
-        a[i] = r;
-    }
-    a[0] = out(sn, one, sd);
-}
-
-// LDPC_SPA_RWIRE form of check_update_spa_pair<D, false>: the inputs are the clamped
+// Sum-product update of a PAIR of checks held as float2 lanes (.x = check 2q, .y = check
+// 2q + 1), every product one packed op for both checks.  The inputs are the clamped
 // ratios R_i = e^{x_i} (ratio_wire), and tanh(x_i/2) = (R_i - 1) / (R_i + 1).  With
 // D_j = prod_{i != j} (R_i + 1) and N_j = prod_{i != j} (R_i - 1), the output ratio
 // (D_j + N_j) / (D_j - N_j) is, expanding both products in the elementary symmetric
@@ -1040,9 +916,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
         __syncthreads();  // staging read before the message initialisation overwrites it
 #pragma unroll
         for (int i = 0; i < VPT; ++i) {
-            const float w = LDPC_SPA_RWIRE && ALGO == 0 && LDPC_SPA_PROD
-                                ? __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[i], -23.0f, 23.0f))
-                                : v2c_wire<ALGO>(L[i]);
+            const float w = v2c_rwire<ALGO>(L[i]);
 #pragma unroll
             for (int j = 0; j < DV; ++j) at(addr(i, j)) = w;
         }
@@ -1065,7 +939,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
         // products -- no v_log_f32 per edge in the check phase, a v_rcp_f32 in place
         // of the v_exp_f32 here.  The posterior (FINAL) is L + sum log2 r_j in the
         // log-domain order, L = log2(E); MC tests post < 1.
-        constexpr bool PROD = LDPC_SPA_PROD && ALGO == 0;
+        constexpr bool PROD = ALGO == 0;
         if constexpr (PROD) {
 #pragma unroll
             for (int i = 0; i < VPT; ++i) L[i] = __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[i], -126.0f, 126.0f));
@@ -1076,7 +950,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
         uint32_t hb = 0u;
         bool hfirst = true;
         auto put_hard = [&](int i, bool h, const uint32_t(&ad)[DV]) {
-            if (!LDPC_ET_DELTA || hfirst || ((hb >> i) & 1u) != (uint32_t)h) {
+            if (hfirst || ((hb >> i) & 1u) != (uint32_t)h) {
 #pragma unroll
                 for (int j = 0; j < DV; ++j) hsb[ad[j] >> 2] = (uint8_t)h;
             }
@@ -1184,7 +1058,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
         auto var_phase = [&](auto final_tag) {
             constexpr bool FINAL = decltype(final_tag)::value;
             int errs = 0;
-            // variables i, i+1 on float2 (packed sums, differences and 1 - e)
+            // variables i, i+1 on float2 (packed sums and differences)
 #pragma unroll
             for (int i = 0; i + 1 < VPT; i += 2) {
                 uint32_t a0[DV], a1[DV];
@@ -1202,7 +1076,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                 if constexpr (!FINAL) {
 #pragma unroll
                     for (int j = 0; j < DV; ++j) {
-                        const float2 w = v2c_wire2<ALGO>(s - cv[j]);
+                        const float2 w = s - cv[j];  // min-sum (sum-product: var_phase_prod)
                         at(a0[j]) = w.x;
                         at(a1[j]) = w.y;
                     }
@@ -1233,7 +1107,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                 for (int j = 0; j < DV; ++j) s += cv[j];
                 if constexpr (!FINAL) {
 #pragma unroll
-                    for (int j = 0; j < DV; ++j) at(a0[j]) = v2c_wire<ALGO>(s - cv[j]);
+                    for (int j = 0; j < DV; ++j) at(a0[j]) = s - cv[j];
                 }
                 if constexpr (!MC) {
                     if (FINAL || ET) pr[i] = s;
@@ -1269,8 +1143,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 #pragma unroll
                 for (int i = 0; i < DC; ++i) x2[i] = pp[i];
                 if constexpr (ALGO == 0) {
-                    if constexpr (LDPC_SPA_RWIRE && PROD) check_update_spa_pair_rwire<DC>(x2);
-                    else check_update_spa_pair<DC, !PROD>(x2);
+                    check_update_spa_pair_rwire<DC>(x2);
                 } else {
                     float xa[DC], xb[DC];
 #pragma unroll
@@ -1286,18 +1159,7 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
                     for (int i = 0; i < DC; ++i) x2[i] = make_float2(xa[i], xb[i]);
                 }
 #pragma unroll
-                for (int i = 0; i < DC; ++i) {
-                    if constexpr (LDPC_CHECK_W64) {
-                        // one ds_write_b64 per edge of the pair: 3 source dwords = 6 cycles per
-                        // 8 bytes, where ds_write_b128 moves 16 bytes in ~13 (MI355X_MICROARCH.md)
-                        const f32x2 v = {x2[i].x, x2[i].y};
-                        asm volatile("ds_write_b64 %0, %1 offset:%2"
-                                     :: "v"((uint32_t)(size_t)(lds_u8 *)(pp + i) - 8u * i), "v"(v), "i"(8 * i)
-                                     : "memory");
-                    } else {
-                        pp[i] = x2[i];
-                    }
-                }
+                for (int i = 0; i < DC; ++i) pp[i] = x2[i];
             }
             if constexpr (ET) {
                 if (!__syncthreads_or(unsat | (it == 0))) break;
@@ -1380,13 +1242,9 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 // SGN (sum-product with early stop): every v->c ratio carries its variable's hard
 // decision in one bit; the pair's parities of those bits are the syndrome of the
 // previous variable phase (returned: 1 = a check of the pair unsatisfied).
-// LDPC_LOC_LSB: the bit is the ratio's mantissa LSB (a relative change of at most 2^-23,
-// far below the rule's ~10-ulp error), so the check rule takes the inputs as they are:
-// the parity is two v_xor3 chains and one OR per pair, and no input needs its sign
-// stripped.  Otherwise the sign bit, stripped before the rule.
-#ifndef LDPC_LOC_LSB
-#define LDPC_LOC_LSB 1
-#endif
+// The bit is the ratio's mantissa LSB (a relative change of at most 2^-23, far below the
+// rule's ~10-ulp error), so the check rule takes the inputs as they are: the parity is two
+// v_xor3 chains and one OR per pair, and no input needs its sign stripped.
 // XOR of the words of entries 0 .. N-1 (N <= D) of one half of x
 template <int N, int D>
 __device__ __forceinline__ uint32_t bits_parity(const float2 (&x)[D], bool hi) {
@@ -1412,19 +1270,10 @@ __device__ __forceinline__ int loc_check_pair(float *msg, int W, int Nc, int i, 
     }
     if constexpr (U % 2) x[D - 1] = *reinterpret_cast<const float2 *>(msg + W + (U / 2) * 4 * Nc + 2 * i);
     int unsat = 0;
-    if constexpr (SGN && LDPC_LOC_LSB) {  // raw parity words: the caller ORs them and tests bit 0 once
+    if constexpr (SGN) {  // raw parity words: the caller ORs them and tests bit 0 once
         // a mixed pair's .x check has D - 1 inputs: its pad slot holds the rule's output for the
         // padding input (an arbitrary LSB), not a variable's decision
         unsat = (int)(bits_parity<MIXED ? D - 1 : D, D>(x, false) | bits_parity<D, D>(x, true));
-    } else if constexpr (SGN) {
-        uint32_t px = 0, py = 0;
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            px ^= __float_as_uint(x[j].x);
-            py ^= __float_as_uint(x[j].y);
-            x[j] = make_float2(fabsf(x[j].x), fabsf(x[j].y));
-        }
-        unsat = (int)((px | py) >> 31);
     }
     if constexpr (ALGO == 0) {
         if constexpr (MIXED) {  // the .x check has D - 1 edges: pad input R = 0
@@ -1516,9 +1365,6 @@ __device__ __forceinline__ uint32_t block_count(int pred, uint32_t *flag, int pa
 // stop and Monte-Carlo +1-3 %; the reverse assignment -2.4 %, odd workgroups at 1 neutral.
 #define LDPC_LOC_PRIO 1
 #endif
-#ifndef LDPC_LOC_BLOCK_ANY
-#define LDPC_LOC_BLOCK_ANY 1  // bp_loc_kernel early stop: block_any (one barrier) for the stop test
-#endif
 
 
 // DVN0 / DVN1: non-local edges per variable of local slot 0 / 1 (max); ABS0 / ABS1: some
@@ -1543,7 +1389,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     // variable's decision XORs its checks' bits of an LDS syndrome (a few atomics once
     // decoding settles) and the next check phase tests that syndrome
     constexpr bool MSET = ET && ALGO == 1;
-    constexpr bool SGN_LSB = ET && ALGO == 0 && LDPC_LOC_LSB;
+    constexpr bool SGN_LSB = ET && ALGO == 0;
     constexpr int VP = 2 * KP;  // variable pairs per thread
     constexpr int DVM = DVN0 > DVN1 ? DVN0 : DVN1;
     constexpr int DVA = DVM > 0 ? DVM : 1;
@@ -1597,7 +1443,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     // the local one spliced in at its index jl (the oracle's order: bit-exact)
     auto ms_sum = [&](auto dn_tag, int v, const float2 &Lv, const float2 &lv, const float2 (&cv)[DVA]) {
         constexpr int DN = decltype(dn_tag)::value;
-        if constexpr (DN == 2 && LDPC_LOC_MS_BFI) {
+        if constexpr (DN == 2) {
             // three terms in order: jl = 0 (ml, n0, n1), 1 (n0, ml, n1), 2 (n0, n1, ml); the masks
             // jl == 0 / jl == 2 are sign-extended one-hot bits of loc_info (v_bfe_i32), the
             // selects v_bfi_b32 -- VALU only, no per-lane masks held in SGPRs
@@ -1756,11 +1602,9 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             if constexpr (SPA) {
                 w = make_float2(__builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].x, -23.0f, 23.0f)),
                                 __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].y, -23.0f, 23.0f)));
-                if constexpr (ET && LDPC_LOC_LSB)  // the channel decision in the LSB
+                if constexpr (ET)  // the channel decision in the LSB
                     w = make_float2(__uint_as_float(bfi_lsb(__float_as_uint(w.x), (uint32_t)(L[v].x < 0.0f))),
                                     __uint_as_float(bfi_lsb(__float_as_uint(w.y), (uint32_t)(L[v].y < 0.0f))));
-                else if constexpr (ET)
-                    w = make_float2(copysignf(w.x, L[v].x), copysignf(w.y, L[v].y));
                 L[v] = make_float2(__builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].x, -126.0f, 126.0f)),
                                    __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(L[v].y, -126.0f, 126.0f)));
             } else {
@@ -1800,7 +1644,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                 if constexpr (DV > 1) pre[1] = pre[0] * loc[v];
 #pragma unroll
                 for (int j = 2; j < DV; ++j) pre[j] = pre[j - 1] * cv[j - 2];
-                uint32_t sx = 0, sy = 0;  // ET: the decision rides in every outgoing sign bit
+                uint32_t sx = 0, sy = 0;  // ET: the decision rides in every outgoing mantissa LSB
                 if constexpr (MC || ET) {
                     // P < 1 on the bits: P is a product of positive clamped ratios, so
                     // bits(P) - bits(1.0) is negative exactly when P < 1 (no compare / select)
@@ -1809,16 +1653,14 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                     const uint32_t dy = (__float_as_uint(P.y) + 0xC0800000u) >> 31;
                     dec = (int)(dx | dy << 1);
                     if constexpr (ET) {
-                        sx = LDPC_LOC_LSB ? dx : dx << 31;
-                        sy = LDPC_LOC_LSB ? dy : dy << 31;
+                        sx = dx;
+                        sy = dy;
                     }
                 }
                 auto sgn = [&](float2 R) {
-                    if constexpr (ET && LDPC_LOC_LSB)  // LSB := decision (one v_bfi_b32 per value)
+                    if constexpr (ET)  // LSB := decision (one v_bfi_b32 per value)
                         return make_float2(__uint_as_float(bfi_lsb(__float_as_uint(R.x), sx)),
                                            __uint_as_float(bfi_lsb(__float_as_uint(R.y), sy)));
-                    if constexpr (ET) return make_float2(__uint_as_float(__float_as_uint(R.x) | sx),
-                                                         __uint_as_float(__float_as_uint(R.y) | sy));
                     return R;
                 };
                 float2 suf = DN > 0 ? cv[DN > 0 ? DN - 1 : 0] : make_float2(1.0f, 1.0f);
@@ -1851,7 +1693,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
         for (; it < iters; ++it) {
             __syncthreads();  // variable phase (or initialisation) complete
             int unsat = 0;
-            if constexpr (LDPC_LOC_LAUNDER_SP) {  // the gathers' unpacked addresses stay in the loop
+            {  // the gathers' unpacked addresses stay in the loop
 #pragma unroll
                 for (int v = 0; v < VP; ++v)
 #pragma unroll
@@ -1903,8 +1745,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                     slab_now = cnt <= (uint32_t)LDPC_LOC_EP_W0 || it == redo_it;
                     if (more && slab_now) slab_it = it;
                 } else {
-                    more = LDPC_LOC_BLOCK_ANY ? block_any(unsat | (it == 0), stop_flag, it & 1)
-                                              : __syncthreads_or(unsat | (it == 0));
+                    more = block_any(unsat | (it == 0), stop_flag, it & 1);
                 }
                 if (!more) {
                     stopped = true;
@@ -2026,23 +1867,16 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             gather(dn_tag, abs_tag, v, spv, cv, a0, a1);
             if constexpr (SPA) {
                 float2 s;
-                if constexpr (LDPC_LOC_POST_LOGE) {
-                    // the channel term from the register-held E = 2^L: log2 E is L to ~1e-7 (no
-                    // second 40 KB read of the codeword's LLRs); a clamped E (|LLR| > 87 nats) takes
-                    // the input value itself
-                    s = make_float2(__builtin_amdgcn_logf(L[v].x), __builtin_amdgcn_logf(L[v].y));
-                    if (fabsf(s.x) >= 125.5f || fabsf(s.y) >= 125.5f) {
-                        const float *lb = a.llr + (size_t)b * n;
-                        const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid);
-                        const int v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
-                        if (fabsf(s.x) >= 125.5f && v0 >= 0) s.x = to_msg<ALGO>(lb[v0]);
-                        if (fabsf(s.y) >= 125.5f && v1 >= 0) s.y = to_msg<ALGO>(lb[v1]);
-                    }
-                } else {
+                // the channel term from the register-held E = 2^L: log2 E is L to ~1e-7 (no
+                // second 40 KB read of the codeword's LLRs); a clamped E (|LLR| > 87 nats) takes
+                // the input value itself
+                s = make_float2(__builtin_amdgcn_logf(L[v].x), __builtin_amdgcn_logf(L[v].y));
+                if (fabsf(s.x) >= 125.5f || fabsf(s.y) >= 125.5f) {
                     const float *lb = a.llr + (size_t)b * n;
-                    const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid), v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
-                    s = make_float2(v0 >= 0 ? to_msg<ALGO>(ld_fresh(lb, v0)) : 0.0f,
-                                    v1 >= 0 ? to_msg<ALGO>(ld_fresh(lb, v1)) : 0.0f);
+                    const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid);
+                    const int v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
+                    if (fabsf(s.x) >= 125.5f && v0 >= 0) s.x = to_msg<ALGO>(lb[v0]);
+                    if (fabsf(s.y) >= 125.5f && v1 >= 0) s.y = to_msg<ALGO>(lb[v1]);
                 }
                 s = s + make_float2(__builtin_amdgcn_logf(loc[v].x), __builtin_amdgcn_logf(loc[v].y));
 #pragma unroll
