@@ -1411,6 +1411,12 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     auto load_sp = [&](int v, int u) {
         return (uint32_t)ld_fresh(a.loc_pos, (v * DVP + u) * T + tid) + base2;
     };
+    // the variable ids of the thread's var pairs (entry 2v + h; -1: none), every load issued
+    // before the first use (one L2 round trip, not one per var pair; Monte-Carlo staging)
+    auto load_vars = [&](int (&vv)[2 * VP]) {
+#pragma unroll
+        for (int i = 0; i < 2 * VP; ++i) vv[i] = ld_fresh(a.loc_var, i * T + tid);
+    };
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
         if constexpr (INF0) inf[2 * k] = (uint32_t)a.loc_info[(2 * k) * T + tid];
@@ -1499,21 +1505,36 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
         uint32_t mk = chm;
         chm = 0u;
         const uint32_t P4 = 4u * (uint32_t)a.loc_P;
+        constexpr int NF = 2;  // flips per trip (1: -0.4 %, 4: -1.5 %, profiles/r05_ab_flip_batch_locvar.txt)
         while (__builtin_amdgcn_ballot_w64(mk != 0u)) {
-            if (mk) {
-                const int bit = __builtin_ctz(mk);
+            // NF flips per trip: every flip's non-local positions loaded before the first use
+            // (one L2 round trip per NF flips; rows u < DVM exist for every var pair, so the
+            // loads need no guard), the 16-bit half by a bit-field extract (no branch)
+            int bit[NF];
+            bool on[NF];
+            uint32_t raw[NF][DVA];
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                bit[f] = mk ? (int)__builtin_ctz(mk) : 0;
+                on[f] = mk != 0u && tid + (bit[f] >> 2) * T < a.loc_P;  // var pair v = bit / 2, pair slot v / 2
                 mk &= mk - 1u;
-                const int v = bit >> 1, h = bit & 1;
-                const int q = tid + (v >> 1) * T;
-                if (q < a.loc_P) {
+            }
+#pragma unroll
+            for (int f = 0; f < NF; ++f)
+#pragma unroll
+                for (int u = 0; u < DVM; ++u) raw[f][u] = (uint32_t)a.loc_pos[((bit[f] >> 1) * DVP + u) * T + tid];
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                if (on[f]) {
+                    const int v = bit[f] >> 1, h = bit[f] & 1;
+                    const int q = tid + (v >> 1) * T;
                     const uint32_t bl = 2u * (uint32_t)q + (uint32_t)h;
                     atomicXor(&syn[bl >> 5], 1u << (bl & 31));
                     const int dn = (v & 1) ? DVN1 : DVN0;
 #pragma unroll
                     for (int u = 0; u < DVM; ++u) {
                         if (u < dn) {
-                            const uint32_t spv = (uint32_t)a.loc_pos[(v * DVP + u) * T + tid] + base2;
-                            uint32_t w = ((h ? pos_hi_x4(spv) : pos_lo_x4(spv)) >> 2) - (uint32_t)lpos0;
+                            uint32_t w = __builtin_amdgcn_ubfe(raw[f][u], 16u * (uint32_t)h, 16u);
                             w = w >= P4 ? w - P4 : w;
                             const uint32_t bn = 2u * (w >> 2) + (w & 1u);
                             atomicXor(&syn[bn >> 5], 1u << (bn & 31));
@@ -1589,10 +1610,18 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             for (int u = 0; u < DVN1; ++u) sp[2 * k + 1][u] = load_sp(2 * k + 1, u);
         }
         float2 L[VP];  // SPA: E = 2^channel (clamped); min-sum: channel LLR
+        if constexpr (MC) {  // (the other decodes measured 0.5 % slower with the batch: registers)
+            int vv[2 * VP];
+            load_vars(vv);
 #pragma unroll
-        for (int v = 0; v < VP; ++v) {
-            const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid), v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
-            L[v] = make_float2(v0 >= 0 ? msg[v0] : 0.0f, v1 >= 0 ? msg[v1] : 0.0f);
+            for (int v = 0; v < VP; ++v)
+                L[v] = make_float2(vv[2 * v] >= 0 ? msg[vv[2 * v]] : 0.0f, vv[2 * v + 1] >= 0 ? msg[vv[2 * v + 1]] : 0.0f);
+        } else {
+#pragma unroll
+            for (int v = 0; v < VP; ++v) {
+                const int v0 = ld_fresh(a.loc_var, (v * 2 + 0) * T + tid), v1 = ld_fresh(a.loc_var, (v * 2 + 1) * T + tid);
+                L[v] = make_float2(v0 >= 0 ? msg[v0] : 0.0f, v1 >= 0 ? msg[v1] : 0.0f);
+            }
         }
         __syncthreads();
         float2 loc[VP];
