@@ -67,3 +67,17 @@ def test_cfg5_waterfall_on_scaling_law():
         assert dev <= math.log(1 + MODEL_TOL) + 3 * sig, (r["param"], fer, law)
         checked += 1
     assert checked >= 4
+
+
+def test_cfg5_first_point_below_1e6_still_on_law():
+    """eps = 0.4185 (law 7.8e-7), the first point below the waterfall band: run to >= 100 frame
+    errors from checkpoints (results/r05_fer_cfg5_ens_n64800_eps0.4185_*.jsonl,
+    results/r05_ck_ens4185/).  It sits on the law within the same band, so no error floor shows
+    above ~6e-7 at n = 64,800 with X = 3 expurgation."""
+    eps_star, alpha, beta = GOLD["calc_threshold_3_6"], GOLD["alpha_3_6"], GOLD["beta_shift_3_6"]
+    deep = [r for r in _points() if 5e-7 <= float(de.scaling_fer(64800, r["param"], eps_star, alpha, beta)) < 1e-6]
+    assert deep, "configs[4] eps = 0.4185 result missing"
+    for r in deep:
+        law = float(de.scaling_fer(64800, r["param"], eps_star, alpha, beta))
+        sig = math.sqrt(max(1e-12, 1.0 - r["fer"]) / r["frame_errors"])
+        assert abs(math.log(r["fer"] / law)) <= math.log(1 + MODEL_TOL) + 3 * sig, (r["param"], r["fer"], law)
