@@ -1239,25 +1239,28 @@ __global__ __launch_bounds__(T) void bp_lds_kernel(BpArgs a) {
 //   ABS: some variables have fewer than DVN+1 edges; their absent edges gather the
 //   neutral value (ratio 1 / sum 0) and write to a private dummy word.
 // ---------------------------------------------------------------------------
-// SGN (sum-product with early stop): every v->c ratio carries its variable's hard
-// decision in one bit; the pair's parities of those bits are the syndrome of the
-// previous variable phase (returned: 1 = a check of the pair unsatisfied).
-// The bit is the ratio's mantissa LSB (a relative change of at most 2^-23, far below the
-// rule's ~10-ulp error), so the check rule takes the inputs as they are: the parity is two
-// v_xor3 chains and one OR per pair, and no input needs its sign stripped.
-// XOR of the words of entries 0 .. N-1 (N <= D) of one half of x
+// SGN (sum-product with early stop): every non-local v->c ratio carries its variable's hard
+// decision in one bit; with the decisions of the pair's two local variables (lpar, from the
+// thread's own decision bits: bit 0 the .x check's, bit 1 the .y check's parity of them) the
+// pair's parities are the syndrome of the previous variable phase (returned: 1 = a check of
+// the pair unsatisfied).  The bit is the ratio's mantissa LSB (a relative change of at most
+// 2^-23, far below the rule's ~10-ulp error), so the check rule takes the inputs as they are:
+// the parity is two v_bitop3 XOR chains and one OR per pair, no input needs its sign stripped,
+// and the local edges (registers) carry no stamp.
+// seed ^ the words of entries 2 .. N-1 (N <= D) of one half of x
 template <int N, int D>
-__device__ __forceinline__ uint32_t bits_parity(const float2 (&x)[D], bool hi) {
+__device__ __forceinline__ uint32_t bits_parity(const float2 (&x)[D], bool hi, uint32_t seed) {
     auto w = [&](int j) { return __float_as_uint(hi ? x[j].y : x[j].x); };
-    uint32_t p = w(0);
-    int j = 1;
+    uint32_t p = seed;
+    int j = 2;
 #pragma unroll
     for (; j + 1 < N; j += 2) p = xor3u(p, w(j), w(j + 1));
     if (j < N) p ^= w(j);
     return p;
 }
 template <int D, int ALGO, bool MIXED = false, bool SGN = false>
-__device__ __forceinline__ int loc_check_pair(float *msg, int W, int Nc, int i, float2 &l0, float2 &l1, float alpha) {
+__device__ __forceinline__ int loc_check_pair(float *msg, int W, int Nc, int i, float2 &l0, float2 &l1, float alpha,
+                                              uint32_t lpar = 0u) {
     constexpr int U = D - 2;
     float2 x[D];
     x[0] = l0;
@@ -1273,7 +1276,7 @@ __device__ __forceinline__ int loc_check_pair(float *msg, int W, int Nc, int i, 
     if constexpr (SGN) {  // raw parity words: the caller ORs them and tests bit 0 once
         // a mixed pair's .x check has D - 1 inputs: its pad slot holds the rule's output for the
         // padding input (an arbitrary LSB), not a variable's decision
-        unsat = (int)(bits_parity<MIXED ? D - 1 : D, D>(x, false) | bits_parity<D, D>(x, true));
+        unsat = (int)(bits_parity<MIXED ? D - 1 : D, D>(x, false, lpar) | bits_parity<D, D>(x, true, lpar >> 1));
     }
     if constexpr (ALGO == 0) {
         if constexpr (MIXED) {  // the .x check has D - 1 edges: pad input R = 0
@@ -1313,13 +1316,13 @@ __device__ __forceinline__ int loc_check_pair(float *msg, int W, int Nc, int i, 
 // code = dy, or dy | dx << 8 for a mixed pair (dx = dy - 1 = DHI - 1 only)
 template <int D, int DHI, int ALGO, bool SGN>
 __device__ __forceinline__ int loc_check_dispatch(int code, float *msg, int W, int Nc, int i, float2 &l0, float2 &l1,
-                                                  float alpha) {
+                                                  float alpha, uint32_t lpar) {
     if constexpr (D == DHI) {
-        if (code >> 8) return loc_check_pair<D, ALGO, true, SGN>(msg, W, Nc, i, l0, l1, alpha);
-        return loc_check_pair<D, ALGO, false, SGN>(msg, W, Nc, i, l0, l1, alpha);
+        if (code >> 8) return loc_check_pair<D, ALGO, true, SGN>(msg, W, Nc, i, l0, l1, alpha, lpar);
+        return loc_check_pair<D, ALGO, false, SGN>(msg, W, Nc, i, l0, l1, alpha, lpar);
     } else {
-        if (code == D) return loc_check_pair<D, ALGO, false, SGN>(msg, W, Nc, i, l0, l1, alpha);
-        return loc_check_dispatch<D + 1, DHI, ALGO, SGN>(code, msg, W, Nc, i, l0, l1, alpha);
+        if (code == D) return loc_check_pair<D, ALGO, false, SGN>(msg, W, Nc, i, l0, l1, alpha, lpar);
+        return loc_check_dispatch<D + 1, DHI, ALGO, SGN>(code, msg, W, Nc, i, l0, l1, alpha, lpar);
     }
 }
 
@@ -1352,6 +1355,9 @@ __device__ __forceinline__ uint32_t block_count(int pred, uint32_t *flag, int pa
     if (threadIdx.x == 0) flag[par ^ 1] = 0u;
     return c;
 }
+#ifndef LDPC_LOC_STAGE_BATCH
+#define LDPC_LOC_STAGE_BATCH 0
+#endif
 #ifndef LDPC_LOC_EP_W0
 #define LDPC_LOC_EP_W0 48  // early stop with posteriors: slab writes after syndromes with <= this many threads unsatisfied
 #endif
@@ -1494,6 +1500,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
     using HB = std::conditional_t<(4 * KP > 32), uint64_t, uint32_t>;
     static_assert(!MSET || sizeof(HB) == 4, "MSET: 32-bit decision word");
     HB hbits = 0;
+    HB lpar = 0;  // SGN: the parity of each check's two local decisions (see bits_parity)
     // MSET: the decisions that changed in a variable phase (chm, bit 2v + h: hbits before XOR
     // after) flip the syndrome bits of their checks -- the local one (pair q = tid + (v/2) T, bit
     // 2q + h) and the non-local ones (from the slot's packed LDS positions, re-read from L2:
@@ -1610,7 +1617,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             for (int u = 0; u < DVN1; ++u) sp[2 * k + 1][u] = load_sp(2 * k + 1, u);
         }
         float2 L[VP];  // SPA: E = 2^channel (clamped); min-sum: channel LLR
-        if constexpr (MC) {  // (the other decodes measured 0.5 % slower with the batch: registers)
+        if constexpr (MC || LDPC_LOC_STAGE_BATCH) {  // (the other decodes measured 0.5 % slower with the batch: registers)
             int vv[2 * VP];
             load_vars(vv);
 #pragma unroll
@@ -1701,7 +1708,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                     if (j < DV - 1) suf = suf * cv[j - 1];
                 }
                 if (ep && slab_now) slab[v * T + tid] = loc[v] * suf;  // prod of the incoming c->v ratios
-                loc[v] = sgn(ratio_wire2(DN > 0 ? L[v] * suf : L[v]));
+                loc[v] = ratio_wire2(DN > 0 ? L[v] * suf : L[v]);  // local edge: its decision is in lpar
             } else {
                 const float2 s = ms_sum(dn_tag, v, L[v], loc[v], cv);
                 if (ep && slab_now) slab[v * T + tid] = s;  // the posterior itself
@@ -1741,7 +1748,8 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                 if (q < a.loc_P) {
                     if constexpr (DLO == DHI) {  // one class: rows of P pairs from word 0
                         unsat |= loc_check_pair<DLO, ALGO, false, ET && SPA>(msg, 0, a.loc_P, q, loc[2 * k],
-                                                                             loc[2 * k + 1], a.alpha);
+                                                                             loc[2 * k + 1], a.alpha,
+                                                                             (uint32_t)(lpar >> (4 * k)));
                     } else {
                         // class of q by selects on the (scalar) class table -- no per-lane
                         // indexing of kernel arguments
@@ -1755,7 +1763,8 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
                             d = in ? a.loc_cls_d[j] : d;
                         }
                         unsat |= loc_check_dispatch<DLO, DHI, ALGO, ET && SPA>(d, msg, W, q1 - q0, q - q0, loc[2 * k],
-                                                                               loc[2 * k + 1], a.alpha);
+                                                                               loc[2 * k + 1], a.alpha,
+                                                                               (uint32_t)(lpar >> (4 * k)));
                     }
                 }
                 if (LDPC_LOC_CGROUP > 0 && k % LDPC_LOC_CGROUP == LDPC_LOC_CGROUP - 1)
@@ -1802,6 +1811,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             if constexpr (ET) {
                 if constexpr (MSET) chm = (uint32_t)(nh ^ hbits);
                 hbits = nh;
+                if constexpr (SGN_LSB) lpar = nh ^ (nh >> 2);  // bit 4k (+1): check 2q (+1)'s local parity
                 if constexpr (MC) {  // pair slots k with tid + k T < P hold variables
                     const int lim = a.loc_P - tid, nk = lim <= 0 ? 0 : min(KP, (lim + T - 1) / T);
                     const HB vm = 4 * nk >= 8 * (int)sizeof(HB) ? ~(HB)0 : (((HB)1 << (4 * nk)) - 1);
