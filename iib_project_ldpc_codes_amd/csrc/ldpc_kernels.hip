@@ -1355,9 +1355,6 @@ __device__ __forceinline__ uint32_t block_count(int pred, uint32_t *flag, int pa
     if (threadIdx.x == 0) flag[par ^ 1] = 0u;
     return c;
 }
-#ifndef LDPC_LOC_STAGE_BATCH
-#define LDPC_LOC_STAGE_BATCH 0
-#endif
 #ifndef LDPC_LOC_EP_W0
 #define LDPC_LOC_EP_W0 48  // early stop with posteriors: slab writes after syndromes with <= this many threads unsatisfied
 #endif
@@ -1617,7 +1614,7 @@ __global__ __launch_bounds__(T, loc_waves_per_simd(T, KP)) void bp_loc_kernel(Bp
             for (int u = 0; u < DVN1; ++u) sp[2 * k + 1][u] = load_sp(2 * k + 1, u);
         }
         float2 L[VP];  // SPA: E = 2^channel (clamped); min-sum: channel LLR
-        if constexpr (MC || LDPC_LOC_STAGE_BATCH) {  // (the other decodes measured 0.5 % slower with the batch: registers)
+        if constexpr (MC) {  // (the other decodes: neutral to 0.5 % slower with the batch, registers)
             int vv[2 * VP];
             load_vars(vv);
 #pragma unroll
