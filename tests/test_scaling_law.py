@@ -70,7 +70,7 @@ def test_cfg5_waterfall_on_scaling_law():
 
 
 def test_cfg5_first_point_below_1e6_still_on_law():
-    """eps = 0.4185 (law 7.8e-7), the first point below the waterfall band: run to >= 100 (161) frame
+    """eps = 0.4185 (law 7.8e-7), the first point below the waterfall band: run to >= 100 (198) frame
     errors from checkpoints (results/r05_fer_cfg5_ens_n64800_eps0.4185_*.jsonl,
     results/r05_ck_ens4185/).  It sits on the law within the same band, so no error floor shows
     above ~6e-7 at n = 64,800 with X = 3 expurgation."""
