@@ -2,7 +2,7 @@
 # GPU box: one FER campaign point (scripts/fer_sweep.py) to STOP frame errors (the reference's
 # stop rule, parallel_simulator.py:198) or SECONDS, checkpointed every round under
 # gpurun_out/ck_<TAG> (seeded from ck_in/<TAG> when present, so a cut-off run resumes).
-#   scripts/r04_fer.sh <cfg3|cfg4|ens> <point> <seed> <stop> <seconds> <tag>
+#   scripts/fer_campaign.sh <cfg3|cfg4|ens> <point> <seed> <stop> <seconds> <tag>
 set -u
 CFG=$1; PT=$2; SEED=$3; STOP=$4; SECS=$5; TAG=$6
 mkdir -p gpurun_out/ck_$TAG
