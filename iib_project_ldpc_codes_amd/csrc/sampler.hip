@@ -109,53 +109,57 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
     }
 }
 
-// Graphs with kSeqMinE (8192) <= n*dv <= kSeqMaxE: sequential-draw sampler, one wave per
-// graph.  The same law -- a uniform socket permutation conditioned on every check
-// being simple -- drawn slot by slot, so a bad check is seen as soon as its last
-// slot is drawn and the attempt stops there (a failing (3,6) attempt at n = 64,800
-// stops after ~1/5 of the graph instead of paying a whole permutation):
-//   * slot x (in order) takes a uniform unused entry of the pool: its words --
-//     word j = word x&3 of Philox ctr {x>>2 | j<<20, tag|att<<2|3, g_lo, g_hi} --
-//     give Lemire draws on [0, R) until one lands on an unused pool index (a
-//     bitmap in LDS); 1024 words without one reject the attempt (probability
-//     < (3/4)^1000);
-//   * the pool starts as all R = E sockets; when R' = ceil(R/4) entries are left
-//     the unused ones are compacted in order into a new pool (global scratch,
-//     the variable_lookup row) with a fresh bitmap, so no draw ever sees more
-//     than 3/4 of its pool used; the last <= kSeqFinal entries are
-//     Fisher-Yates-shuffled by one lane (stream {blk, tag|1<<30|att<<2|3, g});
-//   * up to 256 consecutive slots are drawn per round, the four of block x>>2 by
-//     one lane (one Philox block per lane per word index), against the bitmap of
-//     the slots before the round; LDS atomic ORs mark the picks, and when two
-//     slots picked the same entry the round keeps only the slots below the
-//     second-lowest slot of every such group (the later slots redraw next round
-//     from the updated bitmap -- a slot's result is its first draw not used by an
-//     earlier slot, exactly the sequential process);
-//   * every check whose slots are all drawn is tested (variable ids kept in an
-//     LDS ring of the last kSeqRing slots); a repeat redraws from slot 0 (att+1).
-// ~25.6 KB of LDS per wave at n = 64,800 (the bitmap), so six graphs per CU.
-// The variable side is built with per-variable occurrence counters packed fb bits
-// per variable into the bitmap's LDS (fb = 0: global CAS, sample_emit_var_side).
+// Graphs with kSeqMinE (8192) <= n*dv <= kSeqMaxE: sequential-draw sampler, one attempt per
+// workgroup of kSeqNW waves.  The same law -- a uniform socket permutation conditioned on every
+// check being simple -- drawn slot by slot, so a bad check is seen as soon as its last slot is
+// drawn and the attempt stops there (a failing (3,6) attempt at n = 64,800 stops after ~1/5 of
+// the graph instead of paying a whole permutation):
+//   * slot x (in order) takes a uniform unused entry of the pool: its words -- word j = word
+//     2(j&1) + (x&1) of Philox ctr {x>>1 | (j>>1)<<20, tag|att<<2|3, g_lo, g_hi}, i.e. one block
+//     holds words 2k, 2k+1 of the slot pair x>>1 -- give Lemire draws on [0, R) until one lands
+//     on an unused pool index (a bitmap in LDS); 1024 words without one reject the attempt
+//     (probability < (3/4)^1000);
+//   * the pool starts as all R = E sockets; when R' = ceil(R/4) entries are left the unused ones
+//     are compacted in order into a new pool (global scratch, the variable_lookup row) with a
+//     fresh bitmap, so no draw ever sees more than 3/4 of its pool used; the last <= kSeqFinal
+//     entries are Fisher-Yates-shuffled by one lane (stream {blk, tag|1<<30|att<<2|3, g});
+//   * a round draws up to kSeqSlots (256) consecutive slots, two per lane (the pair of one Philox
+//     block: its words 0-1 are both slots' first two words), against the bitmap of the slots
+//     before the round; LDS atomic ORs mark the picks, and when two slots picked the same entry
+//     the round keeps the slots below the lowest slot that saw its bit already set (never fewer
+//     than the round's first slot, which is always right) -- a slot's result is its first draw
+//     not used by an earlier slot, so the later slots simply redraw next round from the updated
+//     bitmap: exactly the sequential process, for any atomic order (tests/test_seq_sampler_rounds.py);
+//   * every check whose slots are all drawn is tested (variable ids kept in an LDS ring of the
+//     last kSeqRing slots); a repeat rejects the attempt (att+1).
+// LDS per attempt at n = 64,800: the bitmap (24.3 KB) + ring, retry lists and sync words (2.4 KB),
+// so six attempts -- twelve waves -- per CU.  The waves of an attempt meet at two LDS-only
+// barriers per round (draws | marks | cut), two more in the rare rounds with a collision.
+// The variable side is built with per-variable occurrence counters packed fb bits per variable
+// into the bitmap's LDS (fb = 0: global CAS, sample_emit_var_side).
 // oracle_sample_regular / oracle_sample_csr restate it bit for bit.
-constexpr int kSeqFinal = 64, kSeqRing = 1024;  // ring: a round (<= 512 slots) + the check it completes
-#ifndef LDPC_SEQ_FIRST_WORDS
-#define LDPC_SEQ_FIRST_WORDS 3  // words every slot draws up front (then only ~f^3 of the slots retry)
-#endif
-constexpr int kSeqFirstWords = LDPC_SEQ_FIRST_WORDS;
-#ifndef LDPC_SEQ_WIDE_R
-#define LDPC_SEQ_WIDE_R 0  // > 0: pools of at least this many entries draw 512 slots per round
-#endif                     // (measured slower at n = 64,800: more registers, costlier collisions)
-constexpr int kSeqWideR = LDPC_SEQ_WIDE_R;
-#ifndef LDPC_SEQ_VKEYS
-#define LDPC_SEQ_VKEYS 1  // the attempt's Philox key schedule in VGPRs (PhiloxKeys)
-#endif
+constexpr int kSeqFinal = 64;
+constexpr int kSeqNW = 2;                      // waves per attempt
+constexpr int kSeqT = kSeqNW * kWave;          // threads per attempt
+constexpr int kSeqSlots = 2 * kSeqT;           // slots per round: two per lane
+constexpr int kSeqRing = 512;                  // ring: a round + the longest check it completes
+static_assert(kSeqSlots + kSeqMaxCdeg <= kSeqRing, "the ring must hold a round and the check it completes");
+static_assert(kSeqNW == 2, "the cut words hold two waves");
+// LDS sync words of an attempt: reject flags by round parity, cut[parity][wave], claim broadcast
+enum { kSyFlag = 0, kSyCut = 2, kSyClaim = 8, kSeqSync = 16 };
 
 // LDS ordering between the lanes of one wave (LDS instructions of a wave execute in order):
-// a compiler barrier only -- no s_barrier, no wait for the outstanding global stores that a
-// workgroup-scope fence (__syncthreads) would add to every round
+// a compiler barrier only
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
+}
+// the attempt's waves: an s_barrier ordering LDS only (no wait for outstanding global stores,
+// which a __syncthreads fence would add to every round)
+__device__ __forceinline__ void seq_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 __device__ __forceinline__ int wave_excl_scan(int v, int &total) {
@@ -170,15 +174,18 @@ __device__ __forceinline__ int wave_excl_scan(int v, int &total) {
     return incl - v;
 }
 
-// Shared state of one wave's sequential-draw attempts (LDS pointers, graph id, key).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Shared state of one workgroup's sequential-draw attempts (LDS pointers, graph id, key).
 struct SeqCtx {
     SampleShape sh;
     uint32_t k0, k1, g0, g1;
-    uint32_t mdv;   // regular: socket / dv as a multiply-high by ceil(2^32 / dv) (0: divide)
-    uint32_t *bm;   // [bw] pool bitmap
-    void *ring;     // [kSeqRing] variable of slot x at x % kSeqRing (u16 when n <= 65536, else int)
-    int *fin;       // [kSeqFinal] last pool entries
-    int *tl;        // [2 * kWave] retry task list (second half: writes of lanes without a task)
+    uint32_t mdv;  // regular: socket / dv as a multiply-high by ceil(2^32 / dv) (0: divide)
+    uint32_t *bm;  // [bw] pool bitmap
+    void *ring;    // [kSeqRing] variable of slot x at x % kSeqRing (u16 when n <= 65536, else int)
+    int *fin;      // [kSeqFinal] last pool entries
+    int *tl;       // [kSeqNW][2 * kWave] retry task lists (second half: writes of lanes without a task)
+    int *sy;       // [kSeqSync] sync words
 };
 
 template <bool CSR>
@@ -186,82 +193,59 @@ __device__ __forceinline__ int seq_var_of(const SeqCtx &c, int s) {
     return CSR ? c.sh.vsock[s] : (c.mdv ? (int)__umulhi((uint32_t)s, c.mdv) : s / c.sh.dv);
 }
 
-__device__ __forceinline__ void seq_clear_bm(uint32_t *bm, int words) {
+__device__ __forceinline__ void seq_clear_bm(uint32_t *bm, int words) {  // every thread of the workgroup
     uint4 *b4 = reinterpret_cast<uint4 *>(bm);
-    for (int w = (int)(threadIdx.x & 63); w < (words + 3) >> 2; w += kWave) b4[w] = make_uint4(0u, 0u, 0u, 0u);
-    wave_sync();
+    for (int w = (int)threadIdx.x; w < (words + 3) >> 2; w += (int)blockDim.x) b4[w] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 constexpr uint32_t kSeqNone = 0xFFFFFFFFu;  // search: no simple attempt found (yet)
 
-// Diagnostics build only (-DLDPC_SEQ_STATS=1, scripts/build_variants.sh): the search pass
-// accumulates per-launch counts and s_memtime cycles by phase into g_seq_stats
-// (ldpc_debug_seq_stats); the product build compiles every SEQ_STAT to nothing.
+// Diagnostics build only (-DLDPC_SEQ_STATS=1, scripts/build_sampler_variant.sh): the passes count
+// attempts, rounds, kept slots and collision rounds into g_seq_stats (ldpc_debug_seq_stats);
+// the product build compiles every SEQ_STAT to nothing.
 #ifndef LDPC_SEQ_STATS
 #define LDPC_SEQ_STATS 0
 #endif
-enum SeqStat {
-    kStAttempts, kStAborted, kStRounds, kStKept, kStLaneIters, kStSpreadIters, kStCollRounds, kStProbes,
-    kStCycAttempt, kStCycDraw, kStCycRetry, kStCycMark, kStCycRingVal, kStCycCompact, kStCycClaim, kStValFail,
-    kStCount
-};
+enum SeqStat { kStAttempts, kStAborted, kStRounds, kStKept, kStLaneIters, kStSpreadIters, kStCollRounds, kStValFail,
+               kStCount };
 __device__ unsigned long long g_seq_stats[2 * kStCount];  // search pass, then emit pass
-struct SeqStats {
-    unsigned long long v[kStCount];
-    uint64_t t;  // last time stamp
-    __device__ void zero() {
-        for (int i = 0; i < kStCount; ++i) v[i] = 0;
-        t = __builtin_amdgcn_s_memtime();
-    }
-    __device__ void lap(int i) {  // cycles since the last stamp into v[i]
-        const uint64_t now = __builtin_amdgcn_s_memtime();
-        v[i] += now - t;
-        t = now;
-    }
-    __device__ void flush(int pass = 0) {
-        if ((threadIdx.x & 63) == 0)
-            for (int i = 0; i < kStCount; ++i)
-                if (v[i]) atomicAdd(&g_seq_stats[pass * kStCount + i], v[i]);
-    }
-};
 #if LDPC_SEQ_STATS
-#define SEQ_STAT(st, expr) \
-    do {                   \
-        if (st) { expr; }  \
+#define SEQ_STAT(pass, i, v)                                                                            \
+    do {                                                                                                \
+        if (threadIdx.x == 0) atomicAdd(&g_seq_stats[(pass) * kStCount + (i)], (unsigned long long)(v)); \
     } while (0)
 #else
-#define SEQ_STAT(st, expr) \
-    do {                   \
+#define SEQ_STAT(pass, i, v) \
+    do {                     \
     } while (0)
 #endif
 
-// Attempt `att` of the sequential draw (one wave).  EMIT: every slot's variable also goes to
-// out[x] (the emit pass); otherwise only the verdict matters (the search pass).  pools: >= E
+// Attempt `att` of the sequential draw (the whole workgroup; every return value and loop trip
+// is workgroup-uniform).  out != nullptr: every slot's variable also goes to out[x].  pools: >= E
 // ints of global scratch (the stage pools, two halves used alternately).  best != nullptr
 // (search): the attempt is abandoned once *best (the lowest simple attempt found by any
-// wave) is below att -- it can no longer be the graph's first simple attempt.
-// Returns true when the attempt drew a simple graph.
-template <bool CSR, bool EMIT, typename RT>
-__device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *pools,
-                                            const uint32_t *best, SeqStats *st = nullptr) {
-    const int lane = threadIdx.x & 63;
+// workgroup) is below att -- it can no longer be the graph's first simple attempt.
+// Returns true when the attempt drew a simple graph.  On entry the LDS of the previous attempt
+// may still be read by other waves: the caller has passed a barrier.
+template <bool CSR, typename RT, int PASS>
+__device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *pools, const uint32_t *best) {
+    constexpr int T = kSeqT, S = kSeqSlots;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int E = c.sh.E, m = c.sh.m, dc = c.sh.dc;
-    const uint32_t k0 = c.k0, k1 = c.k1, g0 = c.g0, g1 = c.g1;
-#if LDPC_SEQ_VKEYS
-    const PhiloxKeys K = philox_keys(k0, k1);  // the round loop's Philox keys in VGPRs
-#define LDPC_SEQ_KEYS K
-#else
-#define LDPC_SEQ_KEYS k0, k1
-#endif
+    const uint32_t g0 = c.g0, g1 = c.g1;
+    const PhiloxKeys K = philox_keys(c.k0, c.k1);  // the round loop's Philox keys in VGPRs
     uint32_t *const bm = c.bm;
     RT *const ring = reinterpret_cast<RT *>(c.ring);
-    int *const tl = c.tl;
+    int *const tl = c.tl + wave * 2 * kWave;
+    int *const sy = c.sy;
     const uint32_t c1 = kSampleTag | ((uint32_t)att << 2) | 3u;
-    int R = E, x0 = 0, cdone = 0, nround = 0;
-    uint32_t bseen = kSeqNone;  // search: *best as last loaded
-    bool bad = false;
-    // checks whose slots all lie below `upto`, from cdone on: any repeated variable?
-    auto validate = [&](int upto) -> bool {
+    int R = E, x0 = 0, cdone = 0, nround = 0, par = 0;
+    uint32_t bseen = kSeqNone;  // search (wave 0): *best as last loaded
+    (void)PASS;
+
+    // checks whose slots all lie below `upto`, from cdone on: a repeated variable sets the
+    // reject flag of this round (read by every wave after the next round's first barrier)
+    auto validate = [&](int upto) {
         int cend = cdone;
         if constexpr (CSR) {
             for (;;) {
@@ -270,12 +254,13 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
                 cend += __popcll(f);
                 if (f != ~0ull) break;
             }
+            cend = uni(cend);
         } else {
-            cend = __builtin_amdgcn_readfirstlane(upto / dc);
+            cend = uni(upto / dc);
         }
         bool b = false;
-        for (int cb = cdone; cb < cend; cb += kWave) {
-            const int cc = cb + lane;
+        for (int cb = cdone; cb < cend; cb += T) {
+            const int cc = cb + lane * kSeqNW + wave;  // the waves interleave
             if (cc < cend) {
                 const int lo = CSR ? c.sh.cptr[cc] : cc * dc, d = CSR ? c.sh.cptr[cc + 1] - lo : dc;
                 if (!CSR && d == 6) {  // (3,6): slots in aligned pairs (lo even: no pair straddles the ring's end)
@@ -316,18 +301,15 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
             }
         }
         cdone = cend;
-        return __ballot(b) == 0ull;
+        if (__ballot(b) != 0ull && lane == 0) sy[kSyFlag + par] = 1;
     };
 
     // the rounds of one stage (slots x0 .. xend - 1); POOL: the pool is the global row at
-    // pools + cur (stage 0: the sockets themselves -- the regular form has no global load in
-    // its rounds, so no round waits on earlier stores).  NB: Philox blocks per lane per word
-    // index, i.e. up to 256 NB consecutive slots per round -- lane L draws the four slots of
-    // block x0/4 + L + 64 b (b < NB), relative slot 256 b + 4 L + q.
-    auto rounds = [&](auto pool_tag, auto nb_tag, int xend, int cur) {
+    // pools + cur (stage 0: the sockets themselves -- no global load in its rounds).  Thread tid
+    // draws slots base + 2 tid + q (q = 0, 1) from Philox block (base >> 1) + tid.
+    // Returns false when the attempt is rejected.
+    auto rounds = [&](auto pool_tag, int xend, int cur) -> bool {
         constexpr bool POOL = decltype(pool_tag)::value;
-        constexpr int NB = decltype(nb_tag)::value;
-        constexpr int NS = 4 * NB;  // slots per lane
         const int32_t *pool = pools + cur;
         const uint32_t lt = (0u - (uint32_t)R) % (uint32_t)R;  // Lemire: reject low words below this
         // entry of word w, or -1 when Lemire's test or the bitmap rejects it
@@ -337,229 +319,167 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
             const bool used = (bm[e >> 5] >> (e & 31)) & 1u;
             return ((uint32_t)mm < lt || used) ? -1 : e;
         };
-        auto rel = [&](int k, int l) { return 256 * (k >> 2) + 4 * l + (k & 3); };  // slot k of lane l
-        // The first words of every slot of the round at base bs: the NB x kSeqFirstWords Philox
-        // blocks of the lane, computed round-interleaved (philox_blocks: their ten-step product
-        // chains overlap).  (Computing the next round's blocks in this round's atomics' latency
-        // measured slower: the search pass is issue-bound; scripts/ablations/README.md.)
-        uint4 Wn[NB * kSeqFirstWords];
-        auto first_words = [&](int bs) {
-            uint32_t cc[NB * kSeqFirstWords];
-#pragma unroll
-            for (int b = 0; b < NB; ++b)
-#pragma unroll
-                for (int j = 0; j < kSeqFirstWords; ++j)
-                    cc[b * kSeqFirstWords + j] = ((uint32_t)(bs >> 2) + (uint32_t)(lane + 64 * b)) | ((uint32_t)j << 20);
-            philox_blocks<NB * kSeqFirstWords>(cc, c1, g0, g1, LDPC_SEQ_KEYS, Wn);
-        };
         while (x0 < xend) {
-            if (best && (++nround & 15) == 0) {  // search: a lower simple attempt makes this one moot
+            if (best && wave == 0 && (++nround & 15) == 0) {  // search: a lower simple attempt makes this one moot
                 // (the value loaded 16 rounds ago: the load's latency never stalls a round)
-                if (__builtin_amdgcn_readfirstlane(bseen) < (uint32_t)att) {
-                    SEQ_STAT(st, st->v[kStAborted]++);
-                    bad = true;
-                    return;
-                }
+                if (__builtin_amdgcn_readfirstlane(bseen) < (uint32_t)att && lane == 0) sy[kSyFlag + par] = 1;
                 bseen = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            SEQ_STAT(st, st->v[kStRounds]++; st->lap(kStCycRingVal));
-            // Word j of slot x is word x&3 of Philox {x>>2 | j<<20, c1, g}.  A slot takes its
-            // first word that passes Lemire's test and whose entry is unused (bitmap of the
-            // slots before the round).  Every slot first tries words 0 .. kSeqFirstWords-1 at
-            // once (independent Philox blocks: instruction-level parallelism for a wave that is
-            // mostly waiting, and one LDS round trip for their bitmap reads).  Retries: while
-            // many slots still look, every lane draws the next block of its own slots; once at
-            // most 32 do, the wave spreads them -- L = 2..16 lanes per slot, each trying one of
-            // the slot's next L words, the lowest passing word wins (a slot's words are tried in
-            // order, so the result is the same).
-            const int base = x0 & ~3;
-            uint32_t bb[NB];
+            SEQ_STAT(PASS, kStRounds, 1);
+            const int base = x0 & ~1;
+            const uint32_t blk = (uint32_t)(base >> 1) + (uint32_t)tid;
+            // first two words of both slots: one block
+            const uint4 W0 = philox_block(blk, c1, g0, g1, K);
+            int i[2];
+            bool act[2], need[2];
 #pragma unroll
-            for (int b = 0; b < NB; ++b) bb[b] = (uint32_t)(base >> 2) + (uint32_t)(lane + 64 * b);
-            first_words(base);
-            int i[NS];
-            bool act[NS], need[NS];
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int k = 4 * b + q, x = base + rel(k, lane);
-                    act[k] = x >= x0 && x < xend;
-                    int e[kSeqFirstWords];
-#pragma unroll
-                    for (int j = 0; j < kSeqFirstWords; ++j) e[j] = try_word(pick4(Wn[b * kSeqFirstWords + j], q));
-                    i[k] = e[kSeqFirstWords - 1];
-#pragma unroll
-                    for (int j = kSeqFirstWords - 2; j >= 0; --j) i[k] = e[j] >= 0 ? e[j] : i[k];
-                    need[k] = act[k] && i[k] < 0;
-                }
+            for (int q = 0; q < 2; ++q) {
+                const int x = base + 2 * tid + q;
+                act[q] = x >= x0 && x < xend;
+                const int e0 = try_word(q ? W0.y : W0.x), e1 = try_word(q ? W0.w : W0.z);
+                i[q] = e0 >= 0 ? e0 : e1;
+                need[q] = act[q] && i[q] < 0;
             }
             // later stages: the pool entries of the first draws are loaded now, so the global
             // load's latency overlaps the retries and the marking (a retried slot reloads)
-            int pre[NS];
+            int pre[2] = {0, 0};
             if constexpr (POOL) {
 #pragma unroll
-                for (int k = 0; k < NS; ++k) pre[k] = pool[max(i[k], 0)];
+                for (int q = 0; q < 2; ++q) pre[q] = pool[max(i[q], 0)];
             }
-            SEQ_STAT(st, st->lap(kStCycDraw));
-            bool firstok[NS];  // the slot kept its first draw (no retry): pre[k] is its value
-#pragma unroll
-            for (int k = 0; k < NS; ++k) firstok[k] = !need[k];
-            uint32_t j0 = kSeqFirstWords;  // next word index of every slot still looking
+            const bool firstok0 = !need[0], firstok1 = !need[1];
+            // retries, within the wave: while many slots still look every lane draws the next
+            // block of its own pair; once at most 32 do, the wave spreads them -- L = 2..16 lanes
+            // per slot, each trying one of the slot's next L words, the lowest passing word wins
+            // (a slot's words are tried in order, so the result is the same)
+            uint32_t j0 = 2;  // next word index of every slot still looking (even)
+            bool over = false;
             for (;;) {
-                uint64_t mq[NS];
-                int C = 0;
-#pragma unroll
-                for (int k = 0; k < NS; ++k) {
-                    mq[k] = __ballot(need[k]);
-                    C += __popcll(mq[k]);
-                }
+                const uint64_t mq0 = __ballot(need[0]), mq1 = __ballot(need[1]);
+                const int C = __popcll(mq0) + __popcll(mq1);
                 if (C == 0) break;
-                if (j0 >= 1024u) { bad = true; return; }  // a slot rejected 1024 words: reject the attempt
-                if (C > 32) {  // per lane: the next block of the lane's own slots
-                    SEQ_STAT(st, st->v[kStLaneIters]++);
+                if (j0 >= 1024u) {  // a slot rejected 1024 words: reject the attempt
+                    over = true;
+                    break;
+                }
+                if (C > 32) {
+                    SEQ_STAT(PASS, kStLaneIters, 1);
+                    const uint4 W = philox_block(blk | (j0 << 19), c1, g0, g1, K);  // (j0 >> 1) << 20
 #pragma unroll
-                    for (int b = 0; b < NB; ++b) {
-                        const uint4 W = philox_block(bb[b] | (j0 << 20), c1, g0, g1, LDPC_SEQ_KEYS);
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const int k = 4 * b + q;
-                            const int e = try_word(pick4(W, q));
-                            i[k] = need[k] ? e : i[k];
-                            need[k] = need[k] && e < 0;
-                        }
+                    for (int q = 0; q < 2; ++q) {
+                        int e = try_word(q ? W.y : W.x);
+                        if (e < 0) e = try_word(q ? W.w : W.z);
+                        i[q] = need[q] ? e : i[q];
+                        need[q] = need[q] && e < 0;
                     }
-                    ++j0;
+                    j0 += 2;
                     continue;
                 }
-                SEQ_STAT(st, st->v[kStSpreadIters]++);
-                // spread: slot p (k-major order) gets lanes [p*L, p*L + L), lane p*L + k' tries
+                SEQ_STAT(PASS, kStSpreadIters, 1);
+                // spread: slot p (q-major order) gets lanes [p*L, p*L + L), lane p*L + k' tries
                 // word j0 + k'
                 const int lg1 = C <= 4 ? 4 : (C <= 8 ? 3 : (C <= 16 ? 2 : 1));  // L * C <= 64
                 const int L = 1 << lg1;
                 const uint32_t lmask = (uint32_t)((1ull << L) - 1ull);
-                int pos[NS];
-                int pre = 0;
-#pragma unroll
-                for (int k = 0; k < NS; ++k) {
-                    const uint32_t below =
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(mq[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mq[k], 0u));
-                    pos[k] = pre + (int)below;
-                    pre += __popcll(mq[k]);
-                    tl[need[k] ? pos[k] : kWave + lane] = lane | (k << 6);
-                }
+                const uint32_t b0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(mq0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mq0, 0u));
+                const uint32_t b1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(mq1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mq1, 0u));
+                const int pos[2] = {(int)b0, (int)__popcll(mq0) + (int)b1};
+                tl[need[0] ? pos[0] : kWave + lane] = lane;
+                tl[need[1] ? pos[1] : kWave + lane] = lane | 64;
                 wave_sync();
                 const int p = lane >> lg1, kl = lane & (L - 1);
                 const int ent = tl[p < C ? p : 0];
-                const int own = ent & 63, kk = ent >> 6;
+                const int own = ent & 63, qq = ent >> 6;
                 const uint32_t jj = j0 + (uint32_t)kl;
-                const uint32_t ob = (uint32_t)(base >> 2) + (uint32_t)(own + 64 * (kk >> 2));
-                const uint4 W = philox_block(ob | (jj << 20), c1, g0, g1, LDPC_SEQ_KEYS);
-                const int eh = (p < C && jj < 1024u) ? try_word(pick4(W, kk & 3)) : -1;
+                const uint32_t ob = (uint32_t)(base >> 1) + (uint32_t)(wave * kWave + own);
+                const uint4 W = philox_block(ob | ((jj >> 1) << 20), c1, g0, g1, K);
+                const int eh = (p < C && jj < 1024u) ? try_word(pick4(W, 2 * (int)(jj & 1u) + qq)) : -1;
                 const uint64_t okm = __ballot(eh >= 0);
 #pragma unroll
-                for (int k = 0; k < NS; ++k) {
-                    const int s0 = need[k] ? pos[k] << lg1 : 0;
+                for (int q = 0; q < 2; ++q) {
+                    const int s0 = need[q] ? pos[q] << lg1 : 0;
                     const uint32_t seg = (uint32_t)(okm >> s0) & lmask;
                     const int src = seg ? s0 + (int)__builtin_ctz(seg) : lane;
                     const int got = __shfl(eh, src, kWave);
-                    const bool hit = need[k] && seg != 0u;
-                    i[k] = hit ? got : i[k];
-                    need[k] = need[k] && seg == 0u;
+                    const bool hit = need[q] && seg != 0u;
+                    i[q] = hit ? got : i[q];
+                    need[q] = need[q] && seg == 0u;
                 }
                 j0 += (uint32_t)L;
                 wave_sync();  // tl is rewritten by the next spread
             }
-            SEQ_STAT(st, st->lap(kStCycRetry));
-            int val[NS];
-            bool dup[NS];
+            int val[2];
 #pragma unroll
-            for (int k = 0; k < NS; ++k) {
-                val[k] = 0;
-                if (act[k]) {
-                    if constexpr (POOL) val[k] = firstok[k] ? pre[k] : pool[i[k]];
-                    else val[k] = seq_var_of<CSR>(c, i[k]);
-                }
+            for (int q = 0; q < 2; ++q) {
+                const bool fok = q ? firstok1 : firstok0;
+                const int ii = max(i[q], 0);
+                if constexpr (POOL) val[q] = fok ? pre[q] : pool[ii];
+                else val[q] = seq_var_of<CSR>(c, ii);
             }
-            bool anyd = false;
+            if (over && lane == 0) sy[kSyFlag + par] = 1;
+            seq_sync();  // (A) every wave's draws read the bitmap of the slots before the round
+            if (uni(sy[kSyFlag + (par ^ 1)])) return false;  // the previous round rejected the attempt
+            // mark the picks; a pick whose bit was already set (by another slot of the round)
+            // is a collision, and the round keeps the slots below the lowest such slot
+            bool dup[2];
 #pragma unroll
-            for (int k = 0; k < NS; ++k) {
-                const uint32_t bit = 1u << (i[k] & 31);
-                dup[k] = act[k] && (atomicOr(&bm[i[k] >> 5], bit) & bit) != 0u;
-                anyd |= dup[k];
+            for (int q = 0; q < 2; ++q) {
+                const bool mk = act[q] && !need[q];
+                const uint32_t bit = mk ? 1u << (i[q] & 31) : 0u;
+                const uint32_t old = atomicOr(&bm[mk ? i[q] >> 5 : 0], bit);
+                dup[q] = need[q] || (old & bit) != 0u;  // need: a slot without a word (over)
             }
-            int t = min(256 * NB, xend - base);  // kept: slots base + [x0 - base, t)
-            if (__ballot(anyd)) {
-                SEQ_STAT(st, st->v[kStCollRounds]++);
-                // keep the slots below the second-lowest slot of every group of equal picks (the
-                // first invalid slot of the group; which slot saw the bit set depends on the
-                // atomic order, so each group is found from its members' picks)
-                uint64_t dm[NS];
-#pragma unroll
-                for (int k = 0; k < NS; ++k) dm[k] = __ballot(dup[k]);
-#pragma unroll
-                for (int k = 0; k < NS; ++k) {
-                    while (dm[k]) {
-                        const int ip = __shfl(i[k], (int)__builtin_ctzll(dm[k]), kWave);
-                        int lo1 = 1 << 30, lo2 = 1 << 30;  // the group's two lowest slots
-#pragma unroll
-                        for (int r = 0; r < NS; ++r) {
-                            const uint64_t g = __ballot(act[r] && i[r] == ip);
-                            dm[r] &= ~g;
-                            if (g) {
-                                const int s1 = rel(r, (int)__builtin_ctzll(g));
-                                const uint64_t g2 = g & (g - 1);
-                                const int s2 = g2 ? rel(r, (int)__builtin_ctzll(g2)) : 1 << 30;
-                                if (s1 < lo1) { lo2 = min(lo1, s2); lo1 = s1; }
-                                else lo2 = min(lo2, s1);
-                            }
-                        }
-                        t = __builtin_amdgcn_readfirstlane(min(t, lo2));
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < NS; ++k)  // undo every pick of the round ...
-                    if (act[k] && !dup[k]) atomicAnd(&bm[i[k] >> 5], ~(1u << (i[k] & 31)));
-#pragma unroll
-                for (int k = 0; k < NS; ++k)  // ... and redo the kept ones
-                    if (act[k] && rel(k, lane) < t) atomicOr(&bm[i[k] >> 5], 1u << (i[k] & 31));
+            {
+                const uint64_t d0 = __ballot(dup[0]), d1 = __ballot(dup[1]);
+                int md = S;
+                if (d0) md = 2 * (wave * kWave + (int)__builtin_ctzll(d0));
+                if (d1) md = min(md, 2 * (wave * kWave + (int)__builtin_ctzll(d1)) + 1);
+                if (lane == 0) sy[kSyCut + 2 * par + wave] = md;
             }
-            SEQ_STAT(st, st->lap(kStCycMark));
-            // ring: each block's four slots in one store (base is a multiple of 4); slots below
-            // x0 keep their values, slots at or above t are redrawn (and rewritten) before any
+            // ring: both slots of the pair in one store (base is even); a slot below x0 (x0 odd)
+            // keeps its value, slots at or above the cut are redrawn (and rewritten) before any
             // check that holds them is tested
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                const int p = (base + 256 * b + 4 * lane) & (kSeqRing - 1);
-                int nv[4] = {val[4 * b], val[4 * b + 1], val[4 * b + 2], val[4 * b + 3]};
-                if (b == 0 && (x0 & 3)) {  // the first block has slots below x0 (lane 0): keep their values
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) nv[q] = act[q] ? nv[q] : (int)ring[p + q];
-                }
+            {
+                const int p = (base + 2 * tid) & (kSeqRing - 1);
+                int v0 = val[0];
+                if (tid == 0 && (x0 & 1)) v0 = (int)ring[p];
                 if constexpr (sizeof(RT) == 2)
-                    *reinterpret_cast<uint2 *>(ring + p) =
-                        make_uint2((uint32_t)nv[0] | ((uint32_t)nv[1] << 16), (uint32_t)nv[2] | ((uint32_t)nv[3] << 16));
+                    *reinterpret_cast<uint32_t *>(ring + p) = (uint32_t)v0 | ((uint32_t)val[1] << 16);
                 else
-                    *reinterpret_cast<int4 *>(ring + p) = make_int4(nv[0], nv[1], nv[2], nv[3]);
+                    *reinterpret_cast<int2 *>(ring + p) = make_int2(v0, val[1]);
             }
-            if (EMIT && out) {
+            seq_sync();  // (B) marks, cut words and ring
+            const int tend = min(S, xend - base);
+            int t = min(uni(min(sy[kSyCut + 2 * par], sy[kSyCut + 2 * par + 1])), tend);
+            if (t < tend) {  // a collision: keep the slots below t (at least the first one)
+                SEQ_STAT(PASS, kStCollRounds, 1);
+                t = max(t, x0 - base + 1);
 #pragma unroll
-                for (int k = 0; k < NS; ++k) {
-                    const int s = rel(k, lane);
-                    if (act[k] && s < t) out[base + s] = val[k];
+                for (int q = 0; q < 2; ++q)  // undo every pick of the round ...
+                    if (act[q] && !dup[q]) atomicAnd(&bm[i[q] >> 5], ~(1u << (i[q] & 31)));
+                seq_sync();
+#pragma unroll
+                for (int q = 0; q < 2; ++q)  // ... and redo the kept ones
+                    if (act[q] && !need[q] && 2 * tid + q < t) atomicOr(&bm[i[q] >> 5], 1u << (i[q] & 31));
+                seq_sync();
+            }
+            if (out) {
+                const int s = base + 2 * tid;
+                if (act[0] && act[1] && 2 * tid + 1 < t) {
+                    *reinterpret_cast<int2 *>(out + s) = make_int2(val[0], val[1]);  // s even: 8-byte aligned
+                } else {
+                    if (act[0] && 2 * tid < t) out[s] = val[0];
+                    if (act[1] && 2 * tid + 1 < t) out[s + 1] = val[1];
                 }
             }
-            SEQ_STAT(st, st->v[kStKept] += (unsigned long long)(base + t - x0));
-            x0 = __builtin_amdgcn_readfirstlane(base + t);  // uniform: scalar loop control
-            wave_sync();
-            if (!validate(x0)) {
-                SEQ_STAT(st, st->v[kStValFail]++);
-                bad = true;
-                return;
-            }
+            SEQ_STAT(PASS, kStKept, base + t - x0);
+            x0 = base + t;
+            validate(x0);
+            par ^= 1;
         }
+        return true;
     };
-    // compact the unused entries of the stage's pool (R entries), in order, into dst
+    // compact the unused entries of the stage's pool (R entries), in order, into dst (wave 0)
     auto compact = [&](auto pool_tag, int cur, auto *dst) {
         constexpr bool POOL = decltype(pool_tag)::value;
         const int32_t *pool = pools + cur;
@@ -586,42 +506,35 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
     };
 
     seq_clear_bm(bm, (R + 31) >> 5);
+    if (tid < 4) sy[tid] = tid < 2 ? 0 : S;
+    __syncthreads();
     int cur = -1;  // offset of the current pool in `pools` (-1: stage 0, the sockets)
-    while (R > kSeqFinal && !bad) {
+    while (R > kSeqFinal) {
         const int Rn = (R + 3) >> 2, xend = E - Rn;
-        // wide rounds (two blocks per lane) while the pool is large: the birthday bound lets
-        // ~400 of 512 slots through a round at R ~ 2e5, ~240 of 256 with one block
-        if (kSeqWideR > 0 && R >= kSeqWideR) {
-            if (cur < 0) rounds(bool_c<false>{}, int_c<2>{}, xend, 0);
-            else rounds(bool_c<true>{}, int_c<2>{}, xend, cur);
-        } else {
-            if (cur < 0) rounds(bool_c<false>{}, int_c<1>{}, xend, 0);
-            else rounds(bool_c<true>{}, int_c<1>{}, xend, cur);
+        const bool ok = cur < 0 ? rounds(bool_c<false>{}, xend, 0) : rounds(bool_c<true>{}, xend, cur);
+        if (!ok) return false;
+        if (wave == 0) {
+            if (Rn <= kSeqFinal) {  // the last entries go to LDS
+                if (cur < 0) compact(bool_c<false>{}, 0, c.fin);
+                else compact(bool_c<true>{}, cur, c.fin);
+            } else {  // the next pool: pools[0 ..) and pools[E/2 ..) alternately (R' <= E/4 + 1)
+                const int nx = cur == 0 ? E / 2 : 0;
+                if (cur < 0) compact(bool_c<false>{}, 0, pools + nx);
+                else compact(bool_c<true>{}, cur, pools + nx);
+            }
         }
-        if (bad) break;
-        SEQ_STAT(st, st->lap(kStCycRingVal));
-        if (Rn <= kSeqFinal) {  // the last entries go to LDS
-            if (cur < 0) compact(bool_c<false>{}, 0, c.fin);
-            else compact(bool_c<true>{}, cur, c.fin);
-        } else {  // the next pool: pools[0 ..) and pools[E/2 ..) alternately (R' <= E/4 + 1)
-            const int nx = cur == 0 ? E / 2 : 0;
-            if (cur < 0) compact(bool_c<false>{}, 0, pools + nx);
-            else compact(bool_c<true>{}, cur, pools + nx);
-            cur = nx;
-        }
-        __threadfence_block();
-        __syncthreads();
+        if (Rn > kSeqFinal) cur = cur == 0 ? E / 2 : 0;
+        __syncthreads();  // the new pool (global or LDS) is visible to every wave
         R = Rn;
         seq_clear_bm(bm, (R + 31) >> 5);
-        SEQ_STAT(st, st->lap(kStCycCompact));
+        __syncthreads();
     }
-    if (bad) return false;
-    // last R <= kSeqFinal entries (in fin): Fisher-Yates by lane 0, then the last slots
+    // last R <= kSeqFinal entries (in fin): Fisher-Yates by thread 0, then the last slots
     int *const fin = c.fin;
-    if (R == E && lane < E) fin[lane] = seq_var_of<CSR>(c, lane);  // tiny graphs: no compaction ran
-    wave_sync();
-    if (lane == 0) {
-        BucketRng rng{k0, k1, 0u, c1 | (1u << 30), g0, g1};
+    if (R == E && tid < E) fin[tid] = seq_var_of<CSR>(c, tid);  // tiny graphs: no compaction ran
+    seq_sync();
+    if (tid == 0) {
+        BucketRng rng{c.k0, c.k1, 0u, c1 | (1u << 30), g0, g1};
         for (int a = R - 1; a >= 1; --a) {
             const int j = (int)rng.below((uint32_t)a + 1u);
             const int tmp = fin[a];
@@ -629,71 +542,70 @@ __device__ __forceinline__ bool seq_attempt(const SeqCtx &c, int att, int32_t *o
             fin[j] = tmp;
         }
     }
-    wave_sync();
-    if (lane < R) {
-        const int x = x0 + lane;
-        if (EMIT && out) out[x] = fin[lane];
-        ring[x & (kSeqRing - 1)] = (RT)fin[lane];
+    seq_sync();
+    if (tid < R) {
+        const int x = x0 + tid;
+        if (out) out[x] = fin[tid];
+        ring[x & (kSeqRing - 1)] = (RT)fin[tid];
     }
-    wave_sync();
-    return validate(E);
+    seq_sync();
+    validate(E);
+    seq_sync();
+    return uni(sy[kSyFlag] | sy[kSyFlag + 1]) == 0;
 }
-#undef LDPC_SEQ_KEYS
 
-// Emit pass (and the whole sampler when start == nullptr): one wave per graph draws attempts
-// start[g], start[g] + 1, ... in order until one is simple (start[g] = the first simple attempt
-// found by sample_search_kernel, so normally exactly one attempt), writes its slots to
+// Emit pass (and the whole sampler when start == nullptr): one workgroup per graph draws
+// attempts start[g], start[g] + 1, ... in order until one is simple (start[g] = the first simple
+// attempt found by sample_search_kernel, so normally exactly one attempt), writes its slots to
 // check_lookup[g], then builds the variable side.  attempts[g] = attempts drawn from 0
 // (negative: max_attempts without a simple graph -- then the identity configuration).
-// LDS of a sequential-draw wave: bitmap [bw] | fin [kSeqFinal] | tl [2 kWave] | ring [kSeqRing] RT
+// LDS of an attempt: bitmap [bw] | fin [kSeqFinal] | tl [kSeqNW][2 kWave] | sy [kSeqSync] | ring [kSeqRing] RT
 template <typename RT>
 __host__ __device__ constexpr size_t seq_lds_bytes(int bw) {
-    return (size_t)4 * (bw + kSeqFinal + 2 * kWave) + sizeof(RT) * kSeqRing;
+    return (size_t)4 * (bw + kSeqFinal + 2 * kSeqT + kSeqSync) + sizeof(RT) * kSeqRing;
+}
+
+template <typename RT>
+__device__ __forceinline__ SeqCtx seq_ctx(const SampleShape &sh, uint32_t k0, uint32_t k1, uint64_t gid, uint32_t mdv,
+                                         unsigned char *smem, int bw) {
+    uint32_t *bm = reinterpret_cast<uint32_t *>(smem);
+    int *fin = reinterpret_cast<int *>(bm + bw);
+    int *tl = fin + kSeqFinal;
+    int *sy = tl + 2 * kSeqT;
+    RT *ring = reinterpret_cast<RT *>(sy + kSeqSync);
+    return SeqCtx{sh, k0, k1, (uint32_t)gid, (uint32_t)(gid >> 32), mdv, bm, ring, fin, tl, sy};
 }
 
 template <bool CSR, typename RT>  // CSR: irregular degree structure (sh.vsock / cptr / vptr); RT: ring entries
-__global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
+__global__ __launch_bounds__(kSeqT) void sample_seq_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
                                                            uint64_t first_graph, int32_t *check_lookup,
                                                            int32_t *variable_lookup, int32_t *attempts,
                                                            int max_attempts, int bw, int fb, uint32_t mdv,
                                                            const uint32_t *start, const uint32_t *homewin) {
     extern __shared__ __align__(16) unsigned char smem[];
-    uint32_t *bm = reinterpret_cast<uint32_t *>(smem);  // [bw] pool bitmap, later rank counters
-    int *fin = reinterpret_cast<int *>(bm + bw);        // [kSeqFinal]
-    int *tl = fin + kSeqFinal;                          // [2 * kWave]
-    RT *ring = reinterpret_cast<RT *>(tl + 2 * kWave);  // [kSeqRing]
     const int n = sh.n, E = sh.E, dv = sh.dv, dc = sh.dc;
     constexpr bool csr = CSR;
-    const int lane = threadIdx.x;
-    const uint64_t gid = first_graph + blockIdx.x;
-    const SeqCtx c{sh, k0, k1, (uint32_t)gid, (uint32_t)(gid >> 32), mdv, bm, ring, fin, tl};
+    const int tid = threadIdx.x;
+    const SeqCtx c = seq_ctx<RT>(sh, k0, k1, first_graph + blockIdx.x, mdv, smem, bw);
+    uint32_t *bm = c.bm;
     int32_t *out = check_lookup + (size_t)blockIdx.x * E;
     int32_t *vl = variable_lookup + (size_t)blockIdx.x * E;
 
     int att = start ? (int)min(start[blockIdx.x], (uint32_t)max_attempts) : 0;
     bool ok = false;
     if (homewin && att < max_attempts && homewin[blockIdx.x] == (uint32_t)att) {
-        ok = true;  // the search's home wave drew this attempt into check_lookup[g] already
+        ok = true;  // the search's home workgroup drew this attempt into check_lookup[g] already
         ++att;
     }
     while (!ok && att < max_attempts) {
-#if LDPC_SEQ_STATS
-        SeqStats stats;
-        stats.zero();
-        const uint64_t t_att = __builtin_amdgcn_s_memtime();
-        ok = seq_attempt<CSR, true, RT>(c, att, out, vl, nullptr, &stats);
-        stats.lap(kStCycRingVal);
-        stats.v[kStAttempts]++;
-        stats.v[kStCycAttempt] += __builtin_amdgcn_s_memtime() - t_att;
-        stats.flush(1);
-#else
-        ok = seq_attempt<CSR, true, RT>(c, att, out, vl, nullptr);
-#endif
+        ok = seq_attempt<CSR, RT, 1>(c, att, out, vl, nullptr);
+        SEQ_STAT(1, kStAttempts, 1);
         ++att;
+        __syncthreads();
     }
-    if (attempts && lane == 0) attempts[blockIdx.x] = ok ? att : -att;
+    if (attempts && tid == 0) attempts[blockIdx.x] = ok ? att : -att;
     if (!ok)  // max_attempts without a simple graph: the identity configuration (in-range ids)
-        for (int x = lane; x < E; x += kWave) out[x] = seq_var_of<CSR>(c, x);
+        for (int x = tid; x < E; x += kSeqT) out[x] = seq_var_of<CSR>(c, x);
     __threadfence_block();
     __syncthreads();
     if (fb < 0) return;  // the variable side is built by sample_var_side_kernel
@@ -704,21 +616,19 @@ __global__ __launch_bounds__(kWave) void sample_seq_kernel(SampleShape sh, uint3
     // variable side: occurrence rank of each slot's variable from fb-bit LDS counters
     // (slot order, so rows come out nearly ascending), then a per-row insertion sort
     seq_clear_bm(bm, bw);
+    __syncthreads();
     const uint32_t fmask = (1u << fb) - 1u;
-    for (int xb = 0; xb < E; xb += kWave) {
-        const int x = xb + lane;
-        if (x < E) {
-            const int v = out[x];
-            const uint32_t pos = (uint32_t)v * (uint32_t)fb;
-            const uint32_t old = atomicAdd(&bm[pos >> 5], 1u << (pos & 31));
-            const int rank = (int)((old >> (pos & 31)) & fmask);
-            if (csr) vl[sh.vptr[v] + rank] = x;
-            else vl[(size_t)v * dv + rank] = x / dc;
-        }
+    for (int x = tid; x < E; x += kSeqT) {
+        const int v = out[x];
+        const uint32_t pos = (uint32_t)v * (uint32_t)fb;
+        const uint32_t old = atomicAdd(&bm[pos >> 5], 1u << (pos & 31));
+        const int rank = (int)((old >> (pos & 31)) & fmask);
+        if (csr) vl[sh.vptr[v] + rank] = x;
+        else vl[(size_t)v * dv + rank] = x / dc;
     }
     __threadfence_block();
     __syncthreads();
-    for (int v = lane; v < n; v += kWave) {
+    for (int v = tid; v < n; v += kSeqT) {
         int32_t *r = vl + (csr ? sh.vptr[v] : (size_t)v * dv);
         const int deg = csr ? sh.vptr[v + 1] - sh.vptr[v] : dv;
         for (int x = 1; x < deg; ++x) {
@@ -798,123 +708,111 @@ __global__ __launch_bounds__(T) void sample_var_side_kernel(SampleShape sh, cons
 }
 
 // Search pass: finds, for each of G graphs, its first simple attempt -- the attempt the
-// sequential sampler would return -- with the attempts of a graph spread over waves.
-// Persistent single-wave workgroups; ctl (global): [0] next graph to open, [1] unused,
-// best[G] (kSeqNone: none yet), natt[G] (next attempt index to claim), homewin[G] (the simple
-// attempt the graph's home wave drew into check_lookup[g], kSeqNone: none).  A wave claims attempts of its home graph until the
-// graph has a simple attempt (then opens the next graph); when every graph is open it helps:
-// it probes for a graph still without one and claims that graph's attempts until it has one.  Every attempt below a graph's
-// final best is claimed and runs to completion (an attempt is abandoned only once best is
-// below it), so best = the lowest simple attempt, exactly the sequential result, for any
-// schedule.  Attempts >= max_attempts are never drawn (best stays kSeqNone).  Pool rows (E
-// ints per wave): variable_lookup rows (grid <= G), rebuilt by the variable-side pass.  The
-// wave that opens a graph draws its attempts into check_lookup[g] and records a simple one in
+// sequential sampler would return -- with the attempts of a graph spread over workgroups.
+// Persistent workgroups of kSeqNW waves (one attempt at a time); ctl (global): [0] next graph to
+// open, [1] unused, best[G] (kSeqNone: none yet), natt[G] (next attempt index to claim),
+// homewin[G] (the simple attempt the graph's home workgroup drew into check_lookup[g], kSeqNone:
+// none).  A workgroup claims attempts of its home graph until the graph has a simple attempt
+// (then opens the next graph); when every graph is open it helps: it probes for a graph still
+// without one and claims that graph's attempts until it has one.  Every attempt below a graph's
+// final best is claimed and runs to completion (an attempt is abandoned only once best is below
+// it), so best = the lowest simple attempt, exactly the sequential result, for any schedule.
+// Attempts >= max_attempts are never drawn (best stays kSeqNone).  Pool rows (E ints per
+// workgroup): variable_lookup rows (grid <= G), rebuilt by the variable-side pass.  The workgroup
+// that opens a graph draws its attempts into check_lookup[g] and records a simple one in
 // homewin[g]; the emit pass skips g when homewin[g] == best[g] and redraws attempt best otherwise.
 template <bool CSR, typename RT>
-__global__ __launch_bounds__(kWave) void sample_search_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
+__global__ __launch_bounds__(kSeqT) void sample_search_kernel(SampleShape sh, uint32_t k0, uint32_t k1,
                                                               uint64_t first_graph, int G, int32_t *scratch_a,
                                                               int32_t *scratch_b, uint32_t *ctl, int max_attempts,
                                                               int bw, uint32_t mdv) {
     extern __shared__ __align__(16) unsigned char smem[];
-    uint32_t *bm = reinterpret_cast<uint32_t *>(smem);
-    int *fin = reinterpret_cast<int *>(bm + bw);
-    int *tl = fin + kSeqFinal;
-    RT *ring = reinterpret_cast<RT *>(tl + 2 * kWave);
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t *best = ctl + 2, *natt = ctl + 2 + G, *homewin = ctl + 2 + 2 * G;
     int32_t *pools = scratch_b + (size_t)blockIdx.x * sh.E;  // grid <= G: variable_lookup row w
     const uint32_t um = (uint32_t)max_attempts;
-    int home = -1;         // the graph whose attempts this wave claims
+    SeqCtx c = seq_ctx<RT>(sh, k0, k1, first_graph, mdv, smem, bw);
+    int *const sy = c.sy;
+    int home = -1;         // (wave 0) the graph whose attempts this workgroup claims
     bool helping = false;  // every graph is open: homes are picked among the open ones
     uint32_t probe = (uint32_t)blockIdx.x * 0x9E3779B9u + 0x7F4A7C15u;
     for (;;) {
-        // claim (graph, attempt) on the home graph (lane 0)
-        const uint64_t t_claim = LDPC_SEQ_STATS ? __builtin_amdgcn_s_memtime() : 0;
-        int g = -1, att = 0;
-        if (lane == 0) {
+        // wave 0 claims (graph, attempt) -- lane 0 on the home graph, the wave probing for a new
+        // home when helping -- and hands it to the workgroup through LDS
+        if (wave == 0) {
+            int g = -1, att = 0;
             for (;;) {
-                if (home < 0 && !helping) {
-                    home = (int)atomicAdd(&ctl[0], 1u);
-                    if (home >= G) { home = -1; helping = true; }
-                }
-                if (home < 0) break;  // helping without a home: probe below
-                if (__hip_atomic_load(&best[home], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSeqNone) {
-                    const uint32_t a = atomicAdd(&natt[home], 1u);
-                    if (a < um) { g = home; att = (int)a; break; }
-                }
-                home = -1;  // resolved or out of attempts
-            }
-        }
-        // lane 0's claim, as wave-uniform (scalar) values
-        g = __builtin_amdgcn_readfirstlane(g);
-        att = __builtin_amdgcn_readfirstlane(att);
-        helping = __builtin_amdgcn_readfirstlane((int)helping) != 0;
-        if (g < 0) {
-            // help: probe the graphs from a pseudo-random start (wrapping) for one without a
-            // simple attempt and with attempts left -- 256 graphs per step, their loads issued
-            // together -- and make it the home; none anywhere: this wave is done
-            probe = probe * 1664525u + 1013904223u;
-            const uint32_t start = (uint32_t)(((uint64_t)probe * (uint32_t)G) >> 32);
-            int found = -1;
-            for (uint32_t k = 0; k < (uint32_t)G && found < 0; k += 4 * kWave) {
-                bool open[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const uint32_t off = k + (uint32_t)(u * kWave + lane);
-                    uint32_t cg = start + off;
-                    if (cg >= (uint32_t)G) cg -= (uint32_t)G;
-                    open[u] = off < (uint32_t)G &&
-                              __hip_atomic_load(&best[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSeqNone &&
-                              __hip_atomic_load(&natt[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < um;
-                }
-#pragma unroll
-                for (int u = 0; u < 4 && found < 0; ++u) {
-                    const uint64_t f = __ballot(open[u]);
-                    if (f) {
-                        uint32_t cg = start + k + (uint32_t)(u * kWave) + (uint32_t)__builtin_ctzll(f);
-                        if (cg >= (uint32_t)G) cg -= (uint32_t)G;
-                        found = (int)cg;
+                if (lane == 0) {
+                    for (;;) {
+                        if (home < 0 && !helping) {
+                            home = (int)atomicAdd(&ctl[0], 1u);
+                            if (home >= G) { home = -1; helping = true; }
+                        }
+                        if (home < 0) break;  // helping without a home: probe below
+                        if (__hip_atomic_load(&best[home], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSeqNone) {
+                            const uint32_t a = atomicAdd(&natt[home], 1u);
+                            if (a < um) { g = home; att = (int)a; break; }
+                        }
+                        home = -1;  // resolved or out of attempts
                     }
                 }
+                g = uni(g);
+                att = uni(att);
+                helping = uni((int)helping) != 0;
+                if (g >= 0) break;
+                // help: probe the graphs from a pseudo-random start (wrapping) for one without a
+                // simple attempt and with attempts left -- 256 graphs per step, their loads issued
+                // together -- and make it the home; none anywhere: this workgroup is done
+                probe = probe * 1664525u + 1013904223u;
+                const uint32_t start = (uint32_t)(((uint64_t)probe * (uint32_t)G) >> 32);
+                int found = -1;
+                for (uint32_t k = 0; k < (uint32_t)G && found < 0; k += 4 * kWave) {
+                    bool open[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t off = k + (uint32_t)(u * kWave + lane);
+                        uint32_t cg = start + off;
+                        if (cg >= (uint32_t)G) cg -= (uint32_t)G;
+                        open[u] = off < (uint32_t)G &&
+                                  __hip_atomic_load(&best[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSeqNone &&
+                                  __hip_atomic_load(&natt[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < um;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4 && found < 0; ++u) {
+                        const uint64_t f = __ballot(open[u]);
+                        if (f) {
+                            uint32_t cg = start + k + (uint32_t)(u * kWave) + (uint32_t)__builtin_ctzll(f);
+                            if (cg >= (uint32_t)G) cg -= (uint32_t)G;
+                            found = (int)cg;
+                        }
+                    }
+                }
+                if (found < 0) break;  // nothing left to claim anywhere (g < 0)
+                home = found;
             }
-            if (found < 0) break;  // nothing left to claim anywhere
-            home = found;
-#if LDPC_SEQ_STATS
-            if (lane == 0) atomicAdd(&g_seq_stats[kStProbes], 1ull);
-#endif
-            continue;
+            if (lane == 0) {
+                sy[kSyClaim] = g;
+                sy[kSyClaim + 1] = att;
+                sy[kSyClaim + 2] = helping ? 0 : 1;
+            }
         }
-#if LDPC_SEQ_STATS
-        if (lane == 0) atomicAdd(&g_seq_stats[kStCycClaim], __builtin_amdgcn_s_memtime() - t_claim);
-#else
-        (void)t_claim;
-#endif
+        seq_sync();
+        const int g = uni(sy[kSyClaim]);
+        if (g < 0) break;
+        const int att = uni(sy[kSyClaim + 1]);
+        // the workgroup that opened graph g is the only one writing its check_lookup row: its
+        // attempts draw into it (a simple one is then the graph itself unless a helper's lower
+        // attempt wins -- the emit pass redraws exactly those graphs); helpers only search
+        const bool solo = uni(sy[kSyClaim + 2]) != 0;
         const uint64_t gid = first_graph + (uint64_t)g;
-        const SeqCtx c{sh, k0, k1, (uint32_t)gid, (uint32_t)(gid >> 32), mdv, bm, ring, fin, tl};
-#if LDPC_SEQ_STATS
-        SeqStats stats;
-        stats.zero();
-        SeqStats *stp = &stats;
-#else
-        SeqStats *stp = nullptr;
-#endif
-        const uint64_t t_att = LDPC_SEQ_STATS ? __builtin_amdgcn_s_memtime() : 0;
-        (void)t_att;
-        // the wave that opened graph g is the only one writing its check_lookup row: its attempts
-        // draw into it (a simple one is then the graph itself unless a helper's lower attempt wins
-        // -- the emit pass redraws exactly those graphs); helpers only search
-        const bool solo = !helping;
-        // one instantiation for both roles (out == nullptr: search only): half the code, and a
-        // simpler control-flow graph for the round loop
-        const bool ok = seq_attempt<CSR, true, RT>(c, att, solo ? scratch_a + (size_t)g * sh.E : nullptr, pools,
-                                                   &best[g], stp);
-        SEQ_STAT(stp, stp->lap(kStCycRingVal); stp->v[kStAttempts]++;
-                 stp->v[kStCycAttempt] += __builtin_amdgcn_s_memtime() - t_att; stp->flush());
-        if (ok && lane == 0) {
+        c.g0 = (uint32_t)gid;
+        c.g1 = (uint32_t)(gid >> 32);
+        const bool ok = seq_attempt<CSR, RT, 0>(c, att, solo ? scratch_a + (size_t)g * sh.E : nullptr, pools, &best[g]);
+        SEQ_STAT(0, kStAttempts, 1);
+        if (ok && tid == 0) {
             atomicMin(&best[g], (uint32_t)att);
             if (solo) homewin[g] = (uint32_t)att;
         }
-        __threadfence_block();
         __syncthreads();
     }
 }
@@ -1075,7 +973,7 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
             sh.vsock == nullptr && sh.dv > 1 && sh.dv < 256 ? (uint32_t)((0x100000000ull + sh.dv - 1) / sh.dv) : 0u;
         const uint32_t *start = nullptr, *homewin = nullptr;
         if (ctl) {
-            // search pass: persistent single-wave workgroups, as many as fit the device (LDS
+            // search pass: persistent workgroups of kSeqNW waves, as many as fit the device (LDS
             // bound), at most one pool row each in the 2G rows of the two outputs
             int dev = 0, cus = 0;
             e = hipGetDevice(&dev);
@@ -1091,7 +989,7 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
             if ((e = hipMemsetAsync(ctl + 2 + G, 0, (size_t)4 * G, stream)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(ctl + 2 + 2 * G, 0xFF, (size_t)4 * G, stream)) != hipSuccess) return e;
             // graphs' home waves draw into check_lookup; pool rows: wave w uses variable_lookup row w
-            hipLaunchKernelGGL(sk, dim3(W), dim3(kWave), lds, stream, sh, k0, k1, first_graph, G, check_lookup,
+            hipLaunchKernelGGL(sk, dim3(W), dim3(kSeqT), lds, stream, sh, k0, k1, first_graph, G, check_lookup,
                                variable_lookup, ctl, max_attempts, bw, mdv);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             start = ctl + 2;
@@ -1107,7 +1005,7 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
             V = (int)std::min<size_t>((size_t)sh.n, (size_t)150 * 1024 * 8 / bits) & ~63;
             if (V < 64) V = 0;
         }
-        hipLaunchKernelGGL(kern, dim3(G), dim3(kWave), lds, stream, sh, k0, k1, first_graph,
+        hipLaunchKernelGGL(kern, dim3(G), dim3(kSeqT), lds, stream, sh, k0, k1, first_graph,
                            check_lookup, variable_lookup, attempts, max_attempts, bw, V ? -1 : fbu, mdv, start,
                            homewin);
         if ((e = hipGetLastError()) != hipSuccess || !V) return e;

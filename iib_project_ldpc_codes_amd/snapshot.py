@@ -28,8 +28,11 @@ VERSION = 1
 
 # The device sampler's graph stream (csrc/sampler.hip: which graph trial t gets): a resumed
 # ensemble run must draw its remaining graphs from the stream its first part drew from.
-# Snapshots written before the field existed (round 3) used this same stream.
-SAMPLER_RULE = "one-level-rs<8192<=seq-draw<=393216/philox4x32-10"
+# Round 6 changed the sequential-draw words (one Philox block = two words of a slot pair, was
+# one word of four slots): SAMPLER_RULE_R3 is the stream of rounds 3-5, and of the snapshots
+# written before the field existed (round 3) -- they no longer resume.
+SAMPLER_RULE = "one-level-rs<8192<=seq-draw-pair-words<=393216/philox4x32-10"
+SAMPLER_RULE_R3 = "one-level-rs<8192<=seq-draw<=393216/philox4x32-10"
 
 
 def graph_fingerprint(graph):
@@ -92,7 +95,7 @@ def restore(mc, snap):
     snapshot's next trial index."""
     have = json.loads(json.dumps(snap["config"]))
     if have.get("graph", {}).get("kind") == "ensemble":
-        have["graph"].setdefault("sampler", SAMPLER_RULE)  # pre-field snapshots: the same stream
+        have["graph"].setdefault("sampler", SAMPLER_RULE_R3)  # pre-field snapshots: the round-3 stream
     if have != config(mc) or snap["seed"] != mc.seed:
         raise ValueError("snapshot is of a different run configuration, sampler stream or seed")
     if len(snap["trial_ranges"]) != 1:

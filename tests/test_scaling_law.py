@@ -70,10 +70,12 @@ def test_cfg5_waterfall_on_scaling_law():
 
 
 def test_cfg5_first_point_below_1e6_still_on_law():
-    """eps = 0.4185 (law 7.8e-7), the first point below the waterfall band: run to >= 100 (198) frame
-    errors from checkpoints (results/r05_fer_cfg5_ens_n64800_eps0.4185_*.jsonl,
-    results/r05_ck_ens4185/).  It sits on the law within the same band, so no error floor shows
-    above ~6e-7 at n = 64,800 with X = 3 expurgation."""
+    """eps = 0.4185 (law 7.8e-7), the first point below the waterfall band: run to the reference's
+    200-frame-error stop from checkpoints (rounds 5-6, 2.76e8 trials: FER 7.24e-7;
+    results/r06_fer_cfg5_ens_n64800_eps0.4185_200fe.jsonl, progress in
+    results/r05_fer_cfg5_ens_n64800_eps0.4185_progress.jsonl, checkpoint results/r05_ck_ens4185/).
+    It sits on the law within the same band, so no error floor shows above ~6e-7 at n = 64,800
+    with X = 3 expurgation."""
     eps_star, alpha, beta = GOLD["calc_threshold_3_6"], GOLD["alpha_3_6"], GOLD["beta_shift_3_6"]
     deep = [r for r in _points() if 5e-7 <= float(de.scaling_fer(64800, r["param"], eps_star, alpha, beta)) < 1e-6]
     assert deep, "configs[4] eps = 0.4185 result missing"

@@ -1,11 +1,11 @@
 """The round rule of the sequential-draw sampler (csrc/sampler.hip) restated in Python and checked
 against the sequential definition it must equal (oracle/ldpc_oracle.c seq_attempt): up to 256
-slots (4 per lane) drawn per round against the bitmap of the slots before the round, picks
-marked by atomic OR in an arbitrary lane order, and -- when slots picked the same pool entry --
-only the slots below the second-lowest slot of every such group kept (undo every pick, redo
-the kept ones).  The word
-stream is a stand-in hash (the rule, not Philox, is under test); pools compact at ceil(R/4)
-entries left, the last <= 64 entries are shuffled.  CPU only."""
+slots (two per lane, two waves) drawn per round against the bitmap of the slots before the
+round, picks marked by atomic OR in an arbitrary order, and -- when slots picked the same pool
+entry -- only the slots below the lowest slot that found its bit already set kept (at least the
+round's first slot; undo every pick, redo the kept ones).  The word stream is a stand-in hash
+(the rule, not Philox, is under test); pools compact at ceil(R/4) entries left, the last <= 64
+entries are shuffled.  CPU only."""
 import hashlib
 import random
 
@@ -67,9 +67,9 @@ def sequential(E, var, att):
 
 
 def rounds(E, var, att, order_rng):
-    """The kernel's rounds: lane L owns the 4 slots of block x0/4 + L (slots below x0 are
-    done), i.e. up to 256 slots per round; the picks are marked by four atomic ORs (q = 0..3
-    in program order, lanes in an arbitrary order within each)."""
+    """The kernel's rounds: thread t of the workgroup owns slots base + 2t, base + 2t + 1
+    (base = x0 rounded down to even; slots below x0 are done), i.e. up to 256 slots per round;
+    the picks of both waves are marked by atomic ORs in an arbitrary order."""
     out, cur, R, x0, nrounds = [None] * E, list(var), E, 0, 0
     while R > FINAL:
         Rn = (R + 3) // 4
@@ -77,21 +77,19 @@ def rounds(E, var, att, order_rng):
         bm = [0] * R
         while x0 < xend:
             nrounds += 1
-            base = x0 & ~3
+            base = x0 & ~1
             slots = [s for s in range(256) if x0 <= base + s < xend]
             cand = {s: _draw(att, base + s, R, bm) for s in slots}
+            order = list(slots)
+            order_rng.shuffle(order)
             dup = {}
-            for q in range(4):
-                lanes = [s for s in slots if s % 4 == q]
-                order_rng.shuffle(lanes)
-                for s in lanes:
-                    dup[s] = bm[cand[s]] == 1
-                    bm[cand[s]] = 1
-            t = min(256, xend - base)
-            if any(dup.values()):
-                for p in (s for s in slots if dup[s]):
-                    grp = sorted(s for s in slots if cand[s] == cand[p])
-                    t = min(t, grp[1])
+            for s in order:
+                dup[s] = bm[cand[s]] == 1
+                bm[cand[s]] = 1
+            tend = min(256, xend - base)
+            t = min([s for s in slots if dup[s]], default=tend)
+            if t < tend:
+                t = max(t, x0 - base + 1)  # the round's first slot is always right
                 for s in slots:
                     if not dup[s]:
                         bm[cand[s]] = 0

@@ -174,24 +174,30 @@ def test_resume_on_two_ranks_equals_sequential(tmp_path):
 
 
 def test_ensemble_snapshot_records_sampler_stream():
-    """An ensemble run's snapshot names the device sampler's stream rule; a snapshot written
-    before the field existed (round 3, the same stream) still resumes, another rule does not."""
+    """An ensemble run's snapshot names the device sampler's stream rule; a snapshot of the
+    round 3-5 stream (SAMPLER_RULE_R3, also the one written before the field existed) or of any
+    other rule does not resume."""
     from iib_project_ldpc_codes_amd.montecarlo import MonteCarlo
 
     def executor(first_cw, Bn, stop, counters):
         counters[0] += Bn
 
-    mc = MonteCarlo.ensemble(64800, 3, 6, "bec", 0.42, 200, seed=3, batch=16, expurgation=3, executor=executor)
+    def fresh():
+        return MonteCarlo.ensemble(64800, 3, 6, "bec", 0.42, 200, seed=3, batch=16, expurgation=3, executor=executor)
+
+    mc = fresh()
     mc.run(48, stop_frame_errors=0)
     snap = mc.snapshot()
     assert snap["config"]["graph"]["sampler"] == snapshot.SAMPLER_RULE
+    same = fresh()
+    same.restore(json.loads(json.dumps(snap)))
+    assert same.next_trial() == 48
     old = json.loads(json.dumps(snap))
     del old["config"]["graph"]["sampler"]
-    mc2 = MonteCarlo.ensemble(64800, 3, 6, "bec", 0.42, 200, seed=3, batch=16, expurgation=3, executor=executor)
-    mc2.restore(old)
-    assert mc2.next_trial() == 48
+    r3 = json.loads(json.dumps(snap))
+    r3["config"]["graph"]["sampler"] = snapshot.SAMPLER_RULE_R3
     other = json.loads(json.dumps(snap))
     other["config"]["graph"]["sampler"] = "another-stream"
-    mc3 = MonteCarlo.ensemble(64800, 3, 6, "bec", 0.42, 200, seed=3, batch=16, expurgation=3, executor=executor)
-    with pytest.raises(ValueError):
-        mc3.restore(other)
+    for bad in (old, r3, other):
+        with pytest.raises(ValueError):
+            fresh().restore(bad)
