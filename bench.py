@@ -170,6 +170,72 @@ def cpu_baseline(graph, llr_host, seconds):
     return out
 
 
+DROPIN_NS = (1000, 10000)
+DROPIN_EPS = 0.40
+
+
+def dropin_words(n, count, seed):
+    """BEC channel words of the all-zero codeword (0 / 2 = erased, int32 like
+    parallel_simulator.py:151), synthetic, eps = DROPIN_EPS."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    return np.where(rng.random((count, n)) < DROPIN_EPS, 2, 0).astype(np.int32)
+
+
+def _call_loop(call, words, seconds):
+    """One call per word, cycling through `words`, for `seconds`: (calls, elapsed)."""
+    return _timed(lambda i: (call(words[i % len(words)]), 1)[1], 1, seconds)
+
+
+def dropin_gpu_rates(seconds):
+    """The reference's literal call surface on this library: one message_passing call per word
+    through ctypes with the marshalling of parallel_simulator.py:131-166 (the mirror's
+    regular_LDPC_code.message_pass_decode: int32 copies of the lists and the word, errors[],
+    the call), 50 iterations, at n = 1000 and 10000.  fixed_code: the same lists every call
+    (parallel_simulator.py:354-379, the cached device graph); new_graph_each_call: two codes
+    of the same shape alternating (the ensemble loop, :198-223, re-sends a new code per trial)."""
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    from iib_project_ldpc_codes_amd.parallel_simulator import regular_LDPC_code
+    out = {}
+    for n in DROPIN_NS:
+        ga, gb = (TannerGraph.random_regular(n, DV, DC, seed=s) for s in (1, 2))
+        code = regular_LDPC_code(None, n, ga.k, DV, DC)
+        words = dropin_words(n, 64, 11)
+        lists = [(ga.check_lookup, ga.variable_lookup), (gb.check_lookup, gb.variable_lookup)]
+        code.message_pass_decode(words[0], ITERS, *lists[0])  # graph upload, stream, staging
+        c_fix, e_fix = _call_loop(lambda w: code.message_pass_decode(w, ITERS, *lists[0]), words, seconds)
+        state = [0]
+
+        def alt(w):
+            state[0] ^= 1
+            return code.message_pass_decode(w, ITERS, *lists[state[0]])
+        c_alt, e_alt = _call_loop(alt, words, seconds * 0.5)
+        out[f"n{n}"] = {
+            "fixed_code": {"calls_per_s": c_fix / e_fix, "us_per_call": e_fix / c_fix * 1e6, "calls": c_fix},
+            "new_graph_each_call": {"calls_per_s": c_alt / e_alt, "us_per_call": e_alt / c_alt * 1e6,
+                                    "calls": c_alt}}
+    return out
+
+
+def dropin_reference_rates(seconds):
+    """The reference's own message_passing.c (oracle/_ref/message_passing.so, built unchanged from
+    the reference sources, one host core) driven exactly as parallel_simulator.py:131-166 does
+    (oracle.ref_message_pass_decode: the same marshalling, ct.CDLL per call), on the words and
+    codes of dropin_gpu_rates."""
+    from oracle import oracle
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    if not oracle.ref_available():
+        return None
+    out = {}
+    for n in DROPIN_NS:
+        ga = TannerGraph.random_regular(n, DV, DC, seed=1)
+        words = dropin_words(n, 64, 11)
+        c, e = _call_loop(lambda w: oracle.ref_message_pass_decode(w, ITERS, ga.check_lookup, ga.variable_lookup,
+                                                                    n, ga.k, DV, DC), words, seconds)
+        out[f"n{n}"] = {"calls_per_s": c / e, "us_per_call": e / c * 1e6, "calls": c, "cores": 1}
+    return out
+
+
 def graph_cfg0():
     from iib_project_ldpc_codes_amd.graph import TannerGraph
     return TannerGraph.random_regular(1000, DV, DC, seed=1)
@@ -489,9 +555,20 @@ def main():
         torch.cuda.synchronize()
         extras["ml_n1000_eps0.45"] = {"words_per_s": 32768 / (a.elapsed_time(b) * 1e-3), "batch": 32768}
 
+    dropin = None
+    if rank == 0 and world == 1 and not args.no_extras:
+        dropin = {"what": "one message_passing call per word through ctypes, parallel_simulator.py:131-166 "
+                          "marshalling, (3,6) BEC eps=0.4, 50 iterations, synthetic words",
+                  "gpu": dropin_gpu_rates(2.0)}
+        extras["dropin_message_passing"] = dropin
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(g, llr[:1024].cpu().numpy(), args.cpu_seconds)
+        if dropin is not None:
+            dropin["reference_c_one_core"] = dropin_reference_rates(2.0)
+            for key, ref in (dropin["reference_c_one_core"] or {}).items():
+                gpu = dropin["gpu"][key]["fixed_code"]["calls_per_s"]
+                dropin["gpu"][key]["fixed_code"]["vs_reference_c"] = gpu / ref["calls_per_s"]
 
     hbm_model = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                  "frac": achieved / HBM_PEAK_GBPS, "algorithmic_bytes_per_codeword_iteration": b_it,

@@ -378,7 +378,8 @@ bool build_irr_layout(const HostGraph &h, int &VPT, int &KC, int &DC, int &S, in
     return true;
 }
 
-int device_graph(const HostGraph &h, ldpc_graph **out) {
+// layouts = false: the BEC arrays only (the drop-in message_passing; no soft-decoder layouts)
+int device_graph(const HostGraph &h, ldpc_graph **out, bool layouts = true) {
     int rc = require_device();
     if (rc) return rc;
     ldpc_graph *g = new ldpc_graph();
@@ -395,7 +396,7 @@ int device_graph(const HostGraph &h, ldpc_graph **out) {
     if (e == hipSuccess) e = upload(&g->vchk, h.vchk);
     if (e == hipSuccess && h.consistent) e = upload(&g->vslot, h.vslot);
     int T = 0, VPT = 0;
-    if (e == hipSuccess && h.consistent && h.dv == 3 && h.dc == 6 && lds_shape(h.n, T, VPT) &&
+    if (e == hipSuccess && layouts && h.consistent && h.dv == 3 && h.dc == 6 && lds_shape(h.n, T, VPT) &&
         (size_t)(lds_pair_span(h.m, h.dc) + kLdsDummy) * 4 <= 150 * 1024) {
         std::vector<int32_t> lv, ls;
         build_lane_layout(h, T, VPT, lv, ls);
@@ -407,7 +408,7 @@ int device_graph(const HostGraph &h, ldpc_graph **out) {
     // LDPC_NO_LOC_LAYOUT=1 in the environment: no local-edge layout (tests run the
     // other kernels on the same graphs)
     const char *noloc = getenv("LDPC_NO_LOC_LAYOUT");
-    if (e == hipSuccess && h.consistent && LDPC_LOC_LAYOUT && !(noloc && noloc[0] == '1')) {
+    if (e == hipSuccess && layouts && h.consistent && LDPC_LOC_LAYOUT && !(noloc && noloc[0] == '1')) {
         LocLayout L;
         // threads: 256 for up to 1024 check pairs (4 per thread); (3,6) codes up to 2560 pairs:
         // 512 threads x 5 pairs, two workgroups per CU when both fit the LDS (the bench code:
@@ -440,7 +441,7 @@ int device_graph(const HostGraph &h, ldpc_graph **out) {
             g->loc_abs0 = L.ABS0; g->loc_abs1 = L.ABS1;
         }
     }
-    if (e == hipSuccess && h.consistent && !g->lane_var && LDPC_IRR) {
+    if (e == hipSuccess && layouts && h.consistent && !g->lane_var && LDPC_IRR) {
         std::vector<int32_t> ln, cd;
         int VPT_ = 0, KC = 0, DC = 0, S = 0, P = 0;
         if (build_irr_layout(h, VPT_, KC, DC, S, P, ln, cd)) {
@@ -458,20 +459,20 @@ int device_graph(const HostGraph &h, ldpc_graph **out) {
     return LDPC_OK;
 }
 
-// Drop-in cache: the reference re-sends the same fixed-code lists on every
-// call (parallel_simulator.py:360), so keep the last uploaded graph.
+// Drop-in state (message_passing, one word per call): the reference re-sends the same
+// fixed-code lists on every call (parallel_simulator.py:360, fresh numpy copies each time), so
+// the last lists are kept on the host and compared exactly (memcmp: no hash to collide); their
+// BEC-only device graph, a stream, and pinned staging for the word / error curve in one
+// transfer each way.
 struct DropInCache {
     int n = -1, k = -1, dv = -1, dc = -1, dev = -1;
-    uint64_t hash = 0;
+    std::vector<int32_t> v2c, c2v;  // the lists of the cached graph
     ldpc_graph *g = nullptr;
+    hipStream_t s = nullptr;
+    unsigned char *pin = nullptr, *dbuf = nullptr;  // [word u8 | errors i32 | its i32]
+    size_t bytes = 0;
 };
 DropInCache g_dropin;
-
-uint64_t fnv(const int32_t *p, size_t len, uint64_t h) {
-    const unsigned char *b = reinterpret_cast<const unsigned char *>(p);
-    for (size_t i = 0; i < len * 4; ++i) h = (h ^ b[i]) * 1099511628211ull;
-    return h;
-}
 }  // namespace
 
 extern "C" {
@@ -688,40 +689,80 @@ int ldpc_bec_decode_batch(const int32_t *variable_to_check_list, const int32_t *
 int message_passing(int *Mvc, int iterations, int *variable_to_check_list, int *check_to_variable_list,
                     int *errors, int n, int k, int dv, int dc) {
     if (iterations <= 0) return 0;  // the reference loop body never runs
-    LDPC_REQUIRE(Mvc && errors, "null Mvc / errors");
+    LDPC_REQUIRE(Mvc && errors && variable_to_check_list && check_to_variable_list, "null Mvc / errors / lists");
     LDPC_REQUIRE(n > 0 && dv > 0 && dc > 0 && k >= 0 && k < n, "bad (n, k, dv, dc)");
     int rc = require_device();
     if (rc) return rc;
-    std::vector<uint8_t> w(n);
-    for (int v = 0; v < n; ++v) {
-        LDPC_REQUIRE(Mvc[v] >= 0 && Mvc[v] <= 2, "Mvc value outside {0, 1, 2}");
-        w[v] = (uint8_t)Mvc[v];
-    }
     // One lock across the cache lookup and the decode: another thread replacing the cached
     // graph cannot free it while this call still uses it.
     std::lock_guard<std::mutex> lk(g_mu);
-    {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        const size_t Ev = (size_t)n * dv, Ec = (size_t)(n - k) * dc;
-        uint64_t h = fnv(variable_to_check_list, Ev, 1469598103934665603ull);
-        h = fnv(check_to_variable_list, Ec, h);
-        DropInCache &c = g_dropin;
-        if (!(c.g && c.n == n && c.k == k && c.dv == dv && c.dc == dc && c.dev == dev && c.hash == h)) {
+    DropInCache &c = g_dropin;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const size_t Ev = (size_t)n * dv, Ec = (size_t)(n - k) * dc;
+    const bool same_shape = c.g && c.n == n && c.k == k && c.dv == dv && c.dc == dc && c.dev == dev;
+    if (!(same_shape && !memcmp(c.v2c.data(), variable_to_check_list, Ev * 4) &&
+          !memcmp(c.c2v.data(), check_to_variable_list, Ec * 4))) {
+        HostGraph hg;
+        rc = host_graph_from_lists(variable_to_check_list, check_to_variable_list, n, k, dv, dc, hg);
+        if (rc) return rc;
+        ldpc_graph *g = c.g;
+        if (same_shape && g->consistent == hg.consistent && g->vchk_len == (int)hg.vchk.size()) {
+            // another graph of the same shape (an ensemble run: a new code per trial): new
+            // contents in the same device arrays
+            LDPC_HIP(hipMemcpy(g->cvar, hg.cvar.data(), 4 * hg.cvar.size(), hipMemcpyHostToDevice));
+            LDPC_HIP(hipMemcpy(g->cptr, hg.cptr.data(), 4 * hg.cptr.size(), hipMemcpyHostToDevice));
+            LDPC_HIP(hipMemcpy(g->vptr, hg.vptr.data(), 4 * hg.vptr.size(), hipMemcpyHostToDevice));
+            LDPC_HIP(hipMemcpy(g->vchk, hg.vchk.data(), 4 * hg.vchk.size(), hipMemcpyHostToDevice));
+            if (hg.consistent) LDPC_HIP(hipMemcpy(g->vslot, hg.vslot.data(), 4 * hg.vslot.size(), hipMemcpyHostToDevice));
+            g->max_vdeg = hg.max_vdeg;
+            g->max_cdeg = hg.max_cdeg;
+        } else {
             if (c.g) ldpc_graph_destroy(c.g);
             c.g = nullptr;
-            HostGraph hg;
-            rc = host_graph_from_lists(variable_to_check_list, check_to_variable_list, n, k, dv, dc, hg);
+            if (c.s && c.dev != dev) {  // the stream and buffers belong to the old device
+                (void)hipStreamDestroy(c.s);
+                (void)hipHostFree(c.pin);
+                (void)hipFree(c.dbuf);
+                c.s = nullptr;
+                c.pin = c.dbuf = nullptr;
+                c.bytes = 0;
+            }
+            rc = device_graph(hg, &c.g, false);
             if (rc) return rc;
-            rc = device_graph(hg, &c.g);
-            if (rc) return rc;
-            c.n = n; c.k = k; c.dv = dv; c.dc = dc; c.dev = dev; c.hash = h;
+            c.n = n; c.k = k; c.dv = dv; c.dc = dc; c.dev = dev;
         }
+        c.v2c.assign(variable_to_check_list, variable_to_check_list + Ev);
+        c.c2v.assign(check_to_variable_list, check_to_variable_list + Ec);
     }
-    int32_t it = 0;
-    rc = bec_host_locked(g_dropin.g, w.data(), 1, iterations, errors, &it);
+    if (!c.s) LDPC_HIP(hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking));
+    const size_t wb = ((size_t)n + 15) & ~(size_t)15, eb = (size_t)4 * iterations;
+    const size_t need = wb + eb + 16;
+    if (need > c.bytes) {
+        (void)hipHostFree(c.pin);
+        (void)hipFree(c.dbuf);
+        c.pin = c.dbuf = nullptr;
+        c.bytes = 0;
+        LDPC_HIP(hipHostMalloc(reinterpret_cast<void **>(&c.pin), need, hipHostMallocDefault));
+        LDPC_HIP(hipMalloc(reinterpret_cast<void **>(&c.dbuf), need));
+        c.bytes = need;
+    }
+    uint8_t *pw = c.pin;
+    for (int v = 0; v < n; ++v) {
+        LDPC_REQUIRE(Mvc[v] >= 0 && Mvc[v] <= 2, "Mvc value outside {0, 1, 2}");
+        pw[v] = (uint8_t)Mvc[v];
+    }
+    memcpy(c.pin + wb, errors, eb);  // the reference accumulates into the caller's errors[]
+    LDPC_HIP(hipMemcpyAsync(c.dbuf, c.pin, wb + eb, hipMemcpyHostToDevice, c.s));
+    rc = ldpc_bec_decode_batch_dev(c.g, c.dbuf, 1, iterations, reinterpret_cast<int32_t *>(c.dbuf + wb),
+                                   reinterpret_cast<int32_t *>(c.dbuf + wb + eb), c.s);
     if (rc) return rc;
-    for (int v = 0; v < n; ++v) Mvc[v] = w[v];
+    LDPC_HIP(hipMemcpyAsync(c.pin, c.dbuf, wb + eb + 4, hipMemcpyDeviceToHost, c.s));
+    LDPC_HIP(hipStreamSynchronize(c.s));
+    for (int v = 0; v < n; ++v) Mvc[v] = pw[v];
+    memcpy(errors, c.pin + wb, eb);
+    int32_t it = 0;
+    memcpy(&it, c.pin + wb + eb, 4);
     return it;
 }
 

@@ -15,7 +15,8 @@ L = _native.lib()
 chk = torch.empty((G, n * 3), dtype=torch.int32, device="cuda")
 var = torch.empty_like(chk)
 att = torch.empty(G, dtype=torch.int32, device="cuda")
-st = (ct.c_uint64 * 32)()
+K = 8  # kStCount of csrc/sampler.hip
+st = (ct.c_uint64 * (2 * K))()
 s = torch.cuda.current_stream()
 _native.check(L.ldpc_sample_regular_dev(n, 3, 6, 5, 0, G, chk.data_ptr(), var.data_ptr(), att.data_ptr(),
                                         s.cuda_stream), "sample")
@@ -28,11 +29,9 @@ _native.check(L.ldpc_sample_regular_dev(n, 3, 6, 5, G, G, chk.data_ptr(), var.da
 b.record(s)
 torch.cuda.synchronize()
 _native.check(L.ldpc_debug_seq_stats(st, 0), "stats")
-v = list(st)[:16]
-emit = list(st)[16:]
-names = ["attempts", "aborted", "rounds", "kept", "lane_iters", "spread_iters", "coll_rounds", "probes",
-         "cyc_attempt", "cyc_draw", "cyc_retry", "cyc_mark", "cyc_ringval", "cyc_compact", "cyc_claim", "val_fail"]
-d = dict(zip(names, v))
+names = ["attempts", "aborted", "rounds", "kept", "lane_iters", "spread_iters", "coll_rounds", "val_fail"]
+d = dict(zip(names, list(st)[:K]))
+emit = dict(zip(names, list(st)[K:]))
 ms = a.elapsed_time(b)
 print(f"n={n} G={G} {ms:.2f} ms  {G / ms * 1e3:.0f} graphs/s  mean attempts {att.float().abs().mean().item():.1f}")
 for k in names:
@@ -40,13 +39,7 @@ for k in names:
 R = max(d["rounds"], 1)
 A = max(d["attempts"], 1)
 print(f"  per graph: attempts {d['attempts'] / G:.1f}  rounds {d['rounds'] / G:.0f}  kept/round {d['kept'] / R:.1f}  "
-      f"rounds/attempt {d['rounds'] / A:.1f}  aborted {d['aborted'] / A:.3f}  val_fail/attempt {d['val_fail'] / A:.3f}")
-print(f"  per round: lane iters {d['lane_iters'] / R:.2f}  spread iters {d['spread_iters'] / R:.2f}  "
+      f"rounds/attempt {d['rounds'] / A:.1f}")
+print(f"  per round: lane iters {d['lane_iters'] / R:.3f}  spread iters {d['spread_iters'] / R:.3f}  "
       f"collision rounds {d['coll_rounds'] / R:.3f}")
-tot = sum(d[k] for k in ("cyc_draw", "cyc_retry", "cyc_mark", "cyc_ringval", "cyc_compact"))
-print(f"  cycles per round: total(attempt) {d['cyc_attempt'] / R:.0f}  " + "  ".join(
-      f"{k[4:]} {d[k] / R:.0f}" for k in ("cyc_draw", "cyc_retry", "cyc_mark", "cyc_ringval", "cyc_compact")) +
-      f"  (sum {tot / R:.0f});  claim cycles per attempt {d['cyc_claim'] / A:.0f}  probes {d['probes']}")
-print(f"  emit pass: attempts {emit[0]}  rounds {emit[2]}  cycles per graph {emit[8] / max(G, 1):.0f}  per round "
-      f"{emit[8] / max(emit[2], 1):.0f} (draw {emit[9] / max(emit[2], 1):.0f} retry {emit[10] / max(emit[2], 1):.0f} "
-      f"mark {emit[11] / max(emit[2], 1):.0f} ringval {emit[12] / max(emit[2], 1):.0f} compact {emit[13] / max(emit[2], 1):.0f})")
+print(f"  emit pass: attempts {emit['attempts']}  rounds {emit['rounds']}  kept/round {emit['kept'] / max(emit['rounds'], 1):.1f}")

@@ -74,6 +74,53 @@ def test_dropin_message_passing_matches_reference_golden(lib, golden):
         np.testing.assert_array_equal(errors, c["errors"])
 
 
+def test_dropin_message_passing_graph_changes(lib, golden):
+    """The drop-in's graph cache across code changes: the golden cases in a shuffled order, so
+    consecutive calls switch between codes of the same shape (the ensemble loop's new code per
+    trial, parallel_simulator.py:198-223: device arrays refilled in place) and of other shapes
+    (graph rebuilt), every list a fresh copy; each call still equals the reference's output."""
+    graphs, cases = golden
+    cs = [c for c in cases if graphs[c["gi"]][0] <= 1000]
+    assert len({c["gi"] for c in cs}) >= 2
+    order = np.random.default_rng(7).permutation(len(cs))
+    for j in order:
+        c = cs[j]
+        n, k, dv, dc, v2c, c2v = graphs[c["gi"]]
+        word = np.array(c["word"], dtype="int32")
+        errors = np.zeros(c["max_its"], np.int32) if c["errin"] is None else c["errin"].astype(np.int32).copy()
+        v2c_ = np.array(v2c, np.int32)
+        c2v_ = np.array(c2v, np.int32)
+        it = lib.message_passing(word.ctypes.data, c["max_its"], v2c_.ctypes.data, c2v_.ctypes.data,
+                                 errors.ctypes.data, n, k, dv, dc)
+        assert it == c["it"], (c["gi"], c["max_its"])
+        np.testing.assert_array_equal(word.astype(np.int8), c["out"])
+        if c["errin"] is None:
+            errors = np.insert(errors, 0, int(np.count_nonzero(c["word"] == 2)))
+        np.testing.assert_array_equal(errors, c["errors"])
+
+
+def test_dropin_message_passing_same_shape_codes_alternate(lib):
+    """Two (3,6) n = 1000 codes of one shape, alternating call by call (the ensemble loop's new
+    code per trial re-sent through message_passing): the device arrays are refilled in place
+    and every call equals the oracle's message_passing.c restatement on its own code."""
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    from oracle import oracle
+    codes = [TannerGraph.random_regular(1000, 3, 6, seed=s) for s in (21, 22)]
+    rng = np.random.default_rng(5)
+    for call in range(12):
+        g = codes[call % 2]
+        word = np.where(rng.random(g.n) < 0.42, 2, 0).astype(np.int32)
+        want_w, want_e, want_it = oracle.bec_decode_batch(word[None, :], 50, g.variable_lookup, g.check_lookup,
+                                                          g.n, g.k, 3, 6)
+        errors = np.zeros(50, np.int32)
+        v2c, c2v = np.array(g.variable_lookup, np.int32), np.array(g.check_lookup, np.int32)
+        it = lib.message_passing(word.ctypes.data, 50, v2c.ctypes.data, c2v.ctypes.data, errors.ctypes.data,
+                                 g.n, g.k, 3, 6)
+        assert it == want_it[0], call
+        np.testing.assert_array_equal(word.astype(np.int8), want_w[0])
+        np.testing.assert_array_equal(errors, want_e[0])
+
+
 def test_bec_batch_matches_reference_golden(golden):
     from iib_project_ldpc_codes_amd import decoder
     graphs, cases = golden
