@@ -73,14 +73,14 @@ __device__ __forceinline__ PhiloxKeys philox_keys(uint32_t k0, uint32_t k1) {
     }
     return K;
 }
-template <int NBK>
+template <int NBK, int ROUNDS = 10>
 __device__ __forceinline__ void philox_blocks(const uint32_t (&c0)[NBK], uint32_t c1, uint32_t c2, uint32_t c3,
                                               const PhiloxKeys &K, uint4 (&out)[NBK]) {
     uint32_t a[NBK], b[NBK], c[NBK], d[NBK];
 #pragma unroll
     for (int i = 0; i < NBK; ++i) { a[i] = c0[i]; b[i] = c1; c[i] = c2; d[i] = c3; }
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < ROUNDS; ++r) {
 #pragma unroll
         for (int i = 0; i < NBK; ++i) {
             const uint64_t p0 = (uint64_t)0xD2511F53u * a[i], p1 = (uint64_t)0xCD9E8D57u * c[i];
@@ -93,10 +93,11 @@ __device__ __forceinline__ void philox_blocks(const uint32_t (&c0)[NBK], uint32_
 #pragma unroll
     for (int i = 0; i < NBK; ++i) out[i] = make_uint4(a[i], b[i], c[i], d[i]);
 }
+template <int ROUNDS = 10>
 __device__ __forceinline__ uint4 philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, const PhiloxKeys &K) {
     const uint32_t cc[1] = {c0};
     uint4 o[1];
-    philox_blocks<1>(cc, c1, c2, c3, K, o);
+    philox_blocks<1, ROUNDS>(cc, c1, c2, c3, K, o);
     return o[0];
 }
 

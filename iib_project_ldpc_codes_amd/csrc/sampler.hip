@@ -139,6 +139,10 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
 // into the bitmap's LDS (fb = 0: global CAS, sample_emit_var_side).
 // oracle_sample_regular / oracle_sample_csr restate it bit for bit.
 constexpr int kSeqFinal = 64;
+#ifndef LDPC_SEQ_PHILOX_ROUNDS
+#define LDPC_SEQ_PHILOX_ROUNDS 10  // timing experiments only: the stream (and oracle) are Philox4x32-10
+#endif
+constexpr int kSeqPhiloxRounds = LDPC_SEQ_PHILOX_ROUNDS;
 constexpr int kSeqNW = 2;                      // waves per attempt
 constexpr int kSeqT = kSeqNW * kWave;          // threads per attempt
 constexpr int kSeqSlots = 2 * kSeqT;           // slots per round: two per lane
@@ -147,6 +151,13 @@ static_assert(kSeqSlots + kSeqMaxCdeg <= kSeqRing, "the ring must hold a round a
 static_assert(kSeqNW == 2, "the cut words hold two waves");
 // LDS sync words of an attempt: reject flags by round parity, cut[parity][wave], claim broadcast
 enum { kSyFlag = 0, kSyCut = 2, kSyClaim = 8, kSeqSync = 16 };
+// LDS of an attempt: sy [kSeqSync] | tl [kSeqNW][2 kWave] | fin [kSeqFinal] | ring [kSeqRing] RT | bitmap [bw]
+// (the bitmap last: its LDS address is a constant, folded into the ds instructions' offsets)
+constexpr uint32_t kSeqRingOff = 4u * (kSeqSync + 2 * kSeqT + kSeqFinal);
+template <typename RT>
+__host__ __device__ constexpr uint32_t seq_bm_off() {
+    return kSeqRingOff + (uint32_t)sizeof(RT) * kSeqRing;
+}
 
 // LDS ordering between the lanes of one wave (LDS instructions of a wave execute in order):
 // a compiler barrier only
@@ -175,12 +186,22 @@ __device__ __forceinline__ int wave_excl_scan(int v, int &total) {
 }
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// The bitmap as an LDS byte address: the sampler kernels have no static LDS, so dynamic LDS
+// starts at address 0 (checked at kernel entry) and the bitmap at the constant offset
+// seq_bm_off<RT>() -- entry e's word is one ds instruction with that offset folded in (through
+// the extern array the compiler adds the array's address, 0, with one VALU per access).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ lds_u32 *bm_word(uint32_t bmoff, int e) {
+    return (lds_u32 *)(size_t)(bmoff + (((uint32_t)e >> 3) & ~3u));
+}
 
 // Shared state of one workgroup's sequential-draw attempts (LDS pointers, graph id, key).
 struct SeqCtx {
     SampleShape sh;
     uint32_t k0, k1, g0, g1;
     uint32_t mdv;  // regular: socket / dv as a multiply-high by ceil(2^32 / dv) (0: divide)
+    uint32_t mdc;  // regular: slot / dc likewise (exact below 2^21 for every dc <= 256)
     uint32_t *bm;  // [bw] pool bitmap
     void *ring;    // [kSeqRing] variable of slot x at x % kSeqRing (u16 when n <= 65536, else int)
     int *fin;      // [kSeqFinal] last pool entries
@@ -235,6 +256,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
     const uint32_t g0 = c.g0, g1 = c.g1;
     const PhiloxKeys K = philox_keys(c.k0, c.k1);  // the round loop's Philox keys in VGPRs
     uint32_t *const bm = c.bm;
+    constexpr uint32_t bmo = seq_bm_off<RT>();
     RT *const ring = reinterpret_cast<RT *>(c.ring);
     int *const tl = c.tl + wave * 2 * kWave;
     int *const sy = c.sy;
@@ -243,8 +265,9 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
     uint32_t bseen = kSeqNone;  // search (wave 0): *best as last loaded
     (void)PASS;
 
-    // checks whose slots all lie below `upto`, from cdone on: a repeated variable sets the
-    // reject flag of this round (read by every wave after the next round's first barrier)
+    // checks whose slots all lie below `upto`, from cdone on (one wave per round): a repeated
+    // variable sets the reject flag of this round (read by every wave after the next round's
+    // first barrier)
     auto validate = [&](int upto) {
         int cend = cdone;
         if constexpr (CSR) {
@@ -256,52 +279,66 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             }
             cend = uni(cend);
         } else {
-            cend = uni(upto / dc);
+            cend = uni((int)__umulhi((uint32_t)upto, c.mdc));
         }
-        bool b = false;
-        for (int cb = cdone; cb < cend; cb += T) {
-            const int cc = cb + lane * kSeqNW + wave;  // the waves interleave
-            if (cc < cend) {
-                const int lo = CSR ? c.sh.cptr[cc] : cc * dc, d = CSR ? c.sh.cptr[cc + 1] - lo : dc;
-                if (!CSR && d == 6) {  // (3,6): slots in aligned pairs (lo even: no pair straddles the ring's end)
-                    uint32_t v[6];
+        if (wave == (par & (kSeqNW - 1))) {  // one wave per round, alternating
+            bool b = false;
+            for (int cb = cdone; cb < cend; cb += kWave) {
+                const int cc = cb + lane;
+                if (cc < cend) {
+                    const int lo = CSR ? c.sh.cptr[cc] : cc * dc, d = CSR ? c.sh.cptr[cc + 1] - lo : dc;
+                    if (!CSR && d == 6 && sizeof(RT) == 2) {
+                        // (3,6), u16 ring: the six variables as three u16 pairs (lo even: no pair
+                        // straddles the ring's end); the 15 pairs compared as nine packed XORs
+                        // (each pair within a word, and two words against each other straight
+                        // and half-swapped), a zero half = a repeated variable
+                        const lds_u32 *r32 = (const lds_u32 *)(size_t)kSeqRingOff;  // the ring (see bm_word)
+                        const int p = lo & (kSeqRing - 1);
+                        const uint32_t w0 = r32[p >> 1], w1 = r32[((p + 2) & (kSeqRing - 1)) >> 1],
+                                       w2 = r32[((p + 4) & (kSeqRing - 1)) >> 1];
+                        const uint32_t s0 = __builtin_amdgcn_alignbit(w0, w0, 16), s1 = __builtin_amdgcn_alignbit(w1, w1, 16),
+                                       s2 = __builtin_amdgcn_alignbit(w2, w2, 16);
+                        auto h = [](uint32_t x) { return __builtin_bit_cast(u16x2, x); };
+                        u16x2 mn = __builtin_elementwise_min(h(w0 ^ s0), h(w1 ^ s1));
+                        mn = __builtin_elementwise_min(mn, h(w2 ^ s2));
+                        mn = __builtin_elementwise_min(mn, h(w0 ^ w1));
+                        mn = __builtin_elementwise_min(mn, h(w0 ^ s1));
+                        mn = __builtin_elementwise_min(mn, h(w0 ^ w2));
+                        mn = __builtin_elementwise_min(mn, h(w0 ^ s2));
+                        mn = __builtin_elementwise_min(mn, h(w1 ^ w2));
+                        mn = __builtin_elementwise_min(mn, h(w1 ^ s2));
+                        b |= mn.x == 0 || mn.y == 0;
+                    } else if (!CSR && d == 6) {
+                        int v[6];
 #pragma unroll
-                    for (int u = 0; u < 6; u += 2) {
-                        const int p = (lo + u) & (kSeqRing - 1);
-                        if constexpr (sizeof(RT) == 2) {
-                            const uint32_t w = *reinterpret_cast<const uint32_t *>(ring + p);
-                            v[u] = w & 0xFFFFu;
-                            v[u + 1] = w >> 16;
-                        } else {
-                            const int2 w = *reinterpret_cast<const int2 *>(ring + p);
-                            v[u] = (uint32_t)w.x;
-                            v[u + 1] = (uint32_t)w.y;
+                        for (int u = 0; u < 6; u += 2) {
+                            const int2 w = *reinterpret_cast<const int2 *>(ring + ((lo + u) & (kSeqRing - 1)));
+                            v[u] = w.x;
+                            v[u + 1] = w.y;
                         }
-                    }
-                    uint32_t mn = 0xFFFFFFFFu;  // zero iff two slots hold the same variable
 #pragma unroll
-                    for (int u = 0; u < 6; ++u)
+                        for (int u = 0; u < 6; ++u)
 #pragma unroll
-                        for (int w = u + 1; w < 6; ++w) mn = min(mn, v[u] ^ v[w]);
-                    b |= mn == 0u;
-                } else if (d <= 8) {
-                    int v[8];
+                            for (int w = u + 1; w < 6; ++w) b |= v[u] == v[w];
+                    } else if (d <= 8) {
+                        int v[8];
 #pragma unroll
-                    for (int a = 0; a < 8; ++a) v[a] = a < d ? (int)ring[(lo + a) & (kSeqRing - 1)] : -1 - a;
+                        for (int a = 0; a < 8; ++a) v[a] = a < d ? (int)ring[(lo + a) & (kSeqRing - 1)] : -1 - a;
 #pragma unroll
-                    for (int a = 0; a < 8; ++a)
+                        for (int a = 0; a < 8; ++a)
 #pragma unroll
-                        for (int e = a + 1; e < 8; ++e) b |= v[a] == v[e];
-                } else {
-                    for (int a = 0; a < d && !b; ++a) {
-                        const int va = (int)ring[(lo + a) & (kSeqRing - 1)];
-                        for (int e = a + 1; e < d; ++e) b |= va == (int)ring[(lo + e) & (kSeqRing - 1)];
+                            for (int e = a + 1; e < 8; ++e) b |= v[a] == v[e];
+                    } else {
+                        for (int a = 0; a < d && !b; ++a) {
+                            const int va = (int)ring[(lo + a) & (kSeqRing - 1)];
+                            for (int e = a + 1; e < d; ++e) b |= va == (int)ring[(lo + e) & (kSeqRing - 1)];
+                        }
                     }
                 }
             }
+            if (__ballot(b) != 0ull && lane == 0) sy[kSyFlag + par] = 1;
         }
         cdone = cend;
-        if (__ballot(b) != 0ull && lane == 0) sy[kSyFlag + par] = 1;
     };
 
     // the rounds of one stage (slots x0 .. xend - 1); POOL: the pool is the global row at
@@ -316,7 +353,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
         auto try_word = [&](uint32_t w) -> int {
             const uint64_t mm = (uint64_t)w * (uint32_t)R;
             const int e = (int)(mm >> 32);
-            const bool used = (bm[e >> 5] >> (e & 31)) & 1u;
+            const bool used = (*bm_word(bmo, e) >> (e & 31)) & 1u;
             return ((uint32_t)mm < lt || used) ? -1 : e;
         };
         while (x0 < xend) {
@@ -329,7 +366,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             const int base = x0 & ~1;
             const uint32_t blk = (uint32_t)(base >> 1) + (uint32_t)tid;
             // first two words of both slots: one block
-            const uint4 W0 = philox_block(blk, c1, g0, g1, K);
+            const uint4 W0 = philox_block<kSeqPhiloxRounds>(blk, c1, g0, g1, K);
             int i[2];
             bool act[2], need[2];
 #pragma unroll
@@ -364,7 +401,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 }
                 if (C > 32) {
                     SEQ_STAT(PASS, kStLaneIters, 1);
-                    const uint4 W = philox_block(blk | (j0 << 19), c1, g0, g1, K);  // (j0 >> 1) << 20
+                    const uint4 W = philox_block<kSeqPhiloxRounds>(blk | (j0 << 19), c1, g0, g1, K);  // (j0 >> 1) << 20
 #pragma unroll
                     for (int q = 0; q < 2; ++q) {
                         int e = try_word(q ? W.y : W.x);
@@ -392,7 +429,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 const int own = ent & 63, qq = ent >> 6;
                 const uint32_t jj = j0 + (uint32_t)kl;
                 const uint32_t ob = (uint32_t)(base >> 1) + (uint32_t)(wave * kWave + own);
-                const uint4 W = philox_block(ob | ((jj >> 1) << 20), c1, g0, g1, K);
+                const uint4 W = philox_block<kSeqPhiloxRounds>(ob | ((jj >> 1) << 20), c1, g0, g1, K);
                 const int eh = (p < C && jj < 1024u) ? try_word(pick4(W, 2 * (int)(jj & 1u) + qq)) : -1;
                 const uint64_t okm = __ballot(eh >= 0);
 #pragma unroll
@@ -426,7 +463,8 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             for (int q = 0; q < 2; ++q) {
                 const bool mk = act[q] && !need[q];
                 const uint32_t bit = mk ? 1u << (i[q] & 31) : 0u;
-                const uint32_t old = atomicOr(&bm[mk ? i[q] >> 5 : 0], bit);
+                const uint32_t old =
+                    __hip_atomic_fetch_or(bm_word(bmo, mk ? i[q] : 0), bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 dup[q] = need[q] || (old & bit) != 0u;  // need: a slot without a word (over)
             }
             {
@@ -456,11 +494,15 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 t = max(t, x0 - base + 1);
 #pragma unroll
                 for (int q = 0; q < 2; ++q)  // undo every pick of the round ...
-                    if (act[q] && !dup[q]) atomicAnd(&bm[i[q] >> 5], ~(1u << (i[q] & 31)));
+                    if (act[q] && !dup[q])
+                        __hip_atomic_fetch_and(bm_word(bmo, i[q]), ~(1u << (i[q] & 31)), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
                 seq_sync();
 #pragma unroll
                 for (int q = 0; q < 2; ++q)  // ... and redo the kept ones
-                    if (act[q] && !need[q] && 2 * tid + q < t) atomicOr(&bm[i[q] >> 5], 1u << (i[q] & 31));
+                    if (act[q] && !need[q] && 2 * tid + q < t)
+                        __hip_atomic_fetch_or(bm_word(bmo, i[q]), 1u << (i[q] & 31), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
                 seq_sync();
             }
             if (out) {
@@ -559,7 +601,6 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
 // attempt found by sample_search_kernel, so normally exactly one attempt), writes its slots to
 // check_lookup[g], then builds the variable side.  attempts[g] = attempts drawn from 0
 // (negative: max_attempts without a simple graph -- then the identity configuration).
-// LDS of an attempt: bitmap [bw] | fin [kSeqFinal] | tl [kSeqNW][2 kWave] | sy [kSeqSync] | ring [kSeqRing] RT
 template <typename RT>
 __host__ __device__ constexpr size_t seq_lds_bytes(int bw) {
     return (size_t)4 * (bw + kSeqFinal + 2 * kSeqT + kSeqSync) + sizeof(RT) * kSeqRing;
@@ -568,12 +609,16 @@ __host__ __device__ constexpr size_t seq_lds_bytes(int bw) {
 template <typename RT>
 __device__ __forceinline__ SeqCtx seq_ctx(const SampleShape &sh, uint32_t k0, uint32_t k1, uint64_t gid, uint32_t mdv,
                                          unsigned char *smem, int bw) {
-    uint32_t *bm = reinterpret_cast<uint32_t *>(smem);
-    int *fin = reinterpret_cast<int *>(bm + bw);
-    int *tl = fin + kSeqFinal;
-    int *sy = tl + 2 * kSeqT;
-    RT *ring = reinterpret_cast<RT *>(sy + kSeqSync);
-    return SeqCtx{sh, k0, k1, (uint32_t)gid, (uint32_t)(gid >> 32), mdv, bm, ring, fin, tl, sy};
+    (void)bw;
+    // bm_word: dynamic LDS at LDS address 0 (no static LDS in these kernels)
+    if ((uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char *)smem != 0u) __builtin_trap();
+    int *sy = reinterpret_cast<int *>(smem);
+    int *tl = sy + kSeqSync;
+    int *fin = tl + 2 * kSeqT;
+    RT *ring = reinterpret_cast<RT *>(fin + kSeqFinal);
+    uint32_t *bm = reinterpret_cast<uint32_t *>(ring + kSeqRing);  // last: every other offset is a constant
+    const uint32_t mdc = sh.vsock ? 0u : (uint32_t)((0x100000000ull + (uint32_t)sh.dc - 1u) / (uint32_t)sh.dc);
+    return SeqCtx{sh, k0, k1, (uint32_t)gid, (uint32_t)(gid >> 32), mdv, mdc, bm, ring, fin, tl, sy};
 }
 
 template <bool CSR, typename RT>  // CSR: irregular degree structure (sh.vsock / cptr / vptr); RT: ring entries

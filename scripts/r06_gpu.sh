@@ -4,8 +4,10 @@
 #   scripts/r06_gpu.sh <step> [<step> ...]
 # steps:
 #   samp_tests   sampler parity tests (device == oracle, ensemble MC, peel)
-#   samp_time    sampler timing, this build against build_variants/r5tree (round-5 build)
-#   ens4185      finish the configs[4] eps=0.4185 point from the round-5 tree (its stream)
+#   samp_time    sampler timing, this build against $LIBS (default build_variants/r05.so, the round-5 build)
+#   samp_stats   search-pass counters of a -DLDPC_SEQ_STATS=1 build (build_variants/stats.so)
+#   samp_prof    rocprofv3 kernel trace + PMC passes of one sampler launch (scripts/prof_sampler.sh)
+#   dropin       drop-in message_passing tests + per-call rates (bench.dropin_*_rates)
 #   gputests     the whole -m gpu suite
 #   bench        bench.py (default arguments)
 set -u
@@ -29,14 +31,22 @@ for s in "$@"; do
             tests/test_gpu_fullsize.py::test_cfg5_ensemble_mc_n64800_vs_oracle
         rc=$? ;;
     samp_time)
-        run 600 r06_samp_time.log python scripts/diag/sampler_time.py --sizes ${SIZES:-10000:4096,64800:4096,64800:16384} \
-            iib_project_ldpc_codes_amd/libldpc_mi355x.so build_variants/r5tree/iib_project_ldpc_codes_amd/libldpc_mi355x.so
+        run 600 r06_samp_time.log python scripts/diag/sampler_time.py --sizes ${SIZES:-64800:4096,64800:16384} \
+            iib_project_ldpc_codes_amd/libldpc_mi355x.so ${LIBS:-build_variants/r05.so}
         rc=$? ;;
-    ens4185)
-        (cd build_variants/r5tree && bash scripts/fer_campaign.sh ens 0.4185 21 200 ${ENS_SECS:-600} ens4185)
+    samp_stats)
+        LDPC_LIB_PATH=build_variants/stats.so run 300 r06_samp_stats.log python scripts/diag/seq_stats.py ${N:-64800} ${G:-4096}
+        rc=$? ;;
+    samp_prof)
+        TAG=${TAG:-r06s} N=${N:-64800} G=${G:-4096} run 900 r06_samp_prof.log bash scripts/prof_sampler.sh
+        rc=$? ;;
+    dropin)
+        run 600 r06_dropin.log $PYT tests/test_gpu_parity.py -k dropin
         rc=$?
-        cp -r build_variants/r5tree/gpurun_out/. gpurun_out/r5tree/ 2>/dev/null
-        echo "[ens4185] rc=$rc" ;;
+        if [ $rc -eq 0 ]; then
+            run 300 r06_dropin_time.log python -c "import json, bench; print(json.dumps({'gpu': bench.dropin_gpu_rates(2.0), 'ref': bench.dropin_reference_rates(2.0)}, indent=1))"
+            rc=$?
+        fi ;;
     gputests)
         run 1500 r06_gputests.log $PYT tests -m gpu
         rc=$? ;;
