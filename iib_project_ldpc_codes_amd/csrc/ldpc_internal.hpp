@@ -190,9 +190,9 @@ constexpr int kSeqMinE = 8192, kSeqMaxE = 393216, kSeqMaxCdeg = 192;
 hipError_t launch_sample_regular(int n, int dv, int dc, uint64_t seed, uint64_t first_graph, int G,
                                  int32_t *check_lookup, int32_t *variable_lookup, int32_t *attempts,
                                  int max_attempts, uint32_t *ctl, hipStream_t stream);
-inline size_t sample_ctl_words(int G) { return 2 + 3 * (size_t)G; }
+inline size_t sample_ctl_words(int G) { return 2 + 4 * (size_t)G; }
 // Diagnostics builds (-DLDPC_SEQ_STATS=1): the search and emit passes' per-phase counters
-// (2 x 16 words, see SeqStat in sampler.hip); hipErrorNotSupported in the product build.
+// (2 x kStCount words, see SeqStat in sampler.hip); hipErrorNotSupported in the product build.
 hipError_t seq_stats(uint64_t *out, int reset);
 // Irregular form: socket s of variable d_vsock[s]; check c owns slots [cptr[c], cptr[c+1]);
 // outputs check_var[g][E] and var_slot[g][E] (CSR, each variable's slots ascending).

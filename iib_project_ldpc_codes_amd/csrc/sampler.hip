@@ -143,6 +143,14 @@ constexpr int kSeqFinal = 64;
 #define LDPC_SEQ_PHILOX_ROUNDS 10  // timing experiments only: the stream (and oracle) are Philox4x32-10
 #endif
 constexpr int kSeqPhiloxRounds = LDPC_SEQ_PHILOX_ROUNDS;
+#ifndef LDPC_SEQ_FIRST_BLOCKS
+#define LDPC_SEQ_FIRST_BLOCKS 2  // Philox blocks every slot pair draws up front (2 words per slot each)
+#endif
+constexpr int kSeqFirstBlocks = LDPC_SEQ_FIRST_BLOCKS;
+#ifndef LDPC_SEQ_SPLIT
+#define LDPC_SEQ_SPLIT 4  // a stage ends when ceil(R / LDPC_SEQ_SPLIT) pool entries are left
+#endif
+constexpr int kSeqSplit = LDPC_SEQ_SPLIT;
 constexpr int kSeqNW = 2;                      // waves per attempt
 constexpr int kSeqT = kSeqNW * kWave;          // threads per attempt
 constexpr int kSeqSlots = 2 * kSeqT;           // slots per round: two per lane
@@ -227,7 +235,7 @@ constexpr uint32_t kSeqNone = 0xFFFFFFFFu;  // search: no simple attempt found (
 #ifndef LDPC_SEQ_STATS
 #define LDPC_SEQ_STATS 0
 #endif
-enum SeqStat { kStAttempts, kStAborted, kStRounds, kStKept, kStLaneIters, kStSpreadIters, kStCollRounds, kStValFail,
+enum SeqStat { kStAttempts, kStAborted, kStRounds, kStKept, kStLaneIters, kStSpreadIters, kStCollRounds, kStAbortRounds,
                kStCount };
 __device__ unsigned long long g_seq_stats[2 * kStCount];  // search pass, then emit pass
 #if LDPC_SEQ_STATS
@@ -359,22 +367,40 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
         while (x0 < xend) {
             if (best && wave == 0 && (++nround & 15) == 0) {  // search: a lower simple attempt makes this one moot
                 // (the value loaded 16 rounds ago: the load's latency never stalls a round)
-                if (__builtin_amdgcn_readfirstlane(bseen) < (uint32_t)att && lane == 0) sy[kSyFlag + par] = 1;
+                if (__builtin_amdgcn_readfirstlane(bseen) < (uint32_t)att) {
+                    if (lane == 0) sy[kSyFlag + par] = 1;
+                    SEQ_STAT(PASS, kStAborted, 1);
+                    SEQ_STAT(PASS, kStAbortRounds, nround);
+                }
                 bseen = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             SEQ_STAT(PASS, kStRounds, 1);
             const int base = x0 & ~1;
             const uint32_t blk = (uint32_t)(base >> 1) + (uint32_t)tid;
-            // first two words of both slots: one block
-            const uint4 W0 = philox_block<kSeqPhiloxRounds>(blk, c1, g0, g1, K);
+            // the first 2 kSeqFirstBlocks words of both slots: kSeqFirstBlocks blocks (their
+            // ten-step chains interleaved), all their bitmap reads in one LDS round trip
+            uint4 Wf[kSeqFirstBlocks];
+            {
+                uint32_t cc[kSeqFirstBlocks];
+#pragma unroll
+                for (int f = 0; f < kSeqFirstBlocks; ++f) cc[f] = blk | ((uint32_t)f << 20);
+                philox_blocks<kSeqFirstBlocks, kSeqPhiloxRounds>(cc, c1, g0, g1, K, Wf);
+            }
             int i[2];
             bool act[2], need[2];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const int x = base + 2 * tid + q;
                 act[q] = x >= x0 && x < xend;
-                const int e0 = try_word(q ? W0.y : W0.x), e1 = try_word(q ? W0.w : W0.z);
-                i[q] = e0 >= 0 ? e0 : e1;
+                int e[2 * kSeqFirstBlocks];
+#pragma unroll
+                for (int f = 0; f < kSeqFirstBlocks; ++f) {
+                    e[2 * f] = try_word(q ? Wf[f].y : Wf[f].x);
+                    e[2 * f + 1] = try_word(q ? Wf[f].w : Wf[f].z);
+                }
+                i[q] = e[2 * kSeqFirstBlocks - 1];
+#pragma unroll
+                for (int j = 2 * kSeqFirstBlocks - 2; j >= 0; --j) i[q] = e[j] >= 0 ? e[j] : i[q];
                 need[q] = act[q] && i[q] < 0;
             }
             // later stages: the pool entries of the first draws are loaded now, so the global
@@ -389,7 +415,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             // block of its own pair; once at most 32 do, the wave spreads them -- L = 2..16 lanes
             // per slot, each trying one of the slot's next L words, the lowest passing word wins
             // (a slot's words are tried in order, so the result is the same)
-            uint32_t j0 = 2;  // next word index of every slot still looking (even)
+            uint32_t j0 = 2 * kSeqFirstBlocks;  // next word index of every slot still looking (even)
             bool over = false;
             for (;;) {
                 const uint64_t mq0 = __ballot(need[0]), mq1 = __ballot(need[1]);
@@ -552,20 +578,20 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
     __syncthreads();
     int cur = -1;  // offset of the current pool in `pools` (-1: stage 0, the sockets)
     while (R > kSeqFinal) {
-        const int Rn = (R + 3) >> 2, xend = E - Rn;
+        const int Rn = (R + kSeqSplit - 1) / kSeqSplit, xend = E - Rn;
         const bool ok = cur < 0 ? rounds(bool_c<false>{}, xend, 0) : rounds(bool_c<true>{}, xend, cur);
         if (!ok) return false;
         if (wave == 0) {
             if (Rn <= kSeqFinal) {  // the last entries go to LDS
                 if (cur < 0) compact(bool_c<false>{}, 0, c.fin);
                 else compact(bool_c<true>{}, cur, c.fin);
-            } else {  // the next pool: pools[0 ..) and pools[E/2 ..) alternately (R' <= E/4 + 1)
-                const int nx = cur == 0 ? E / 2 : 0;
+            } else {  // the next pool: pools[0 ..) and pools[ceil(E/2) ..) alternately
+                const int nx = cur == 0 ? (E + 1) / 2 : 0;
                 if (cur < 0) compact(bool_c<false>{}, 0, pools + nx);
                 else compact(bool_c<true>{}, cur, pools + nx);
             }
         }
-        if (Rn > kSeqFinal) cur = cur == 0 ? E / 2 : 0;
+        if (Rn > kSeqFinal) cur = cur == 0 ? (E + 1) / 2 : 0;
         __syncthreads();  // the new pool (global or LDS) is visible to every wave
         R = Rn;
         seq_clear_bm(bm, (R + 31) >> 5);
@@ -773,7 +799,7 @@ __global__ __launch_bounds__(kSeqT) void sample_search_kernel(SampleShape sh, ui
                                                               int bw, uint32_t mdv) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t *best = ctl + 2, *natt = ctl + 2 + G, *homewin = ctl + 2 + 2 * G;
+    uint32_t *best = ctl + 2, *natt = ctl + 2 + G, *homewin = ctl + 2 + 2 * G, *wk = ctl + 2 + 3 * G;
     int32_t *pools = scratch_b + (size_t)blockIdx.x * sh.E;  // grid <= G: variable_lookup row w
     const uint32_t um = (uint32_t)max_attempts;
     SeqCtx c = seq_ctx<RT>(sh, k0, k1, first_graph, mdv, smem, bw);
@@ -792,12 +818,14 @@ __global__ __launch_bounds__(kSeqT) void sample_search_kernel(SampleShape sh, ui
                         if (home < 0 && !helping) {
                             home = (int)atomicAdd(&ctl[0], 1u);
                             if (home >= G) { home = -1; helping = true; }
+                            else atomicAdd(&wk[home], 1u);
                         }
                         if (home < 0) break;  // helping without a home: probe below
                         if (__hip_atomic_load(&best[home], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSeqNone) {
                             const uint32_t a = atomicAdd(&natt[home], 1u);
                             if (a < um) { g = home; att = (int)a; break; }
                         }
+                        atomicSub(&wk[home], 1u);
                         home = -1;  // resolved or out of attempts
                     }
                 }
@@ -805,34 +833,41 @@ __global__ __launch_bounds__(kSeqT) void sample_search_kernel(SampleShape sh, ui
                 att = uni(att);
                 helping = uni((int)helping) != 0;
                 if (g >= 0) break;
-                // help: probe the graphs from a pseudo-random start (wrapping) for one without a
-                // simple attempt and with attempts left -- 256 graphs per step, their loads issued
-                // together -- and make it the home; none anywhere: this workgroup is done
+                // help: probe the graphs from a pseudo-random start (wrapping), 256 per step with
+                // their loads issued together, for graphs without a simple attempt and with
+                // attempts left, and join the one with the fewest workers in the first step that
+                // has any (workers of one graph run attempts past its first simple one until that
+                // one completes: spreading the helpers keeps that waste low); none anywhere:
+                // this workgroup is done
                 probe = probe * 1664525u + 1013904223u;
                 const uint32_t start = (uint32_t)(((uint64_t)probe * (uint32_t)G) >> 32);
                 int found = -1;
                 for (uint32_t k = 0; k < (uint32_t)G && found < 0; k += 4 * kWave) {
-                    bool open[4];
+                    uint32_t key = 0xFFFFFFFFu;  // (workers << 8 | u * 64 + lane... ) of this lane's best open graph
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const uint32_t off = k + (uint32_t)(u * kWave + lane);
                         uint32_t cg = start + off;
                         if (cg >= (uint32_t)G) cg -= (uint32_t)G;
-                        open[u] = off < (uint32_t)G &&
-                                  __hip_atomic_load(&best[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSeqNone &&
-                                  __hip_atomic_load(&natt[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < um;
+                        const bool open =
+                            off < (uint32_t)G &&
+                            __hip_atomic_load(&best[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSeqNone &&
+                            __hip_atomic_load(&natt[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < um;
+                        const uint32_t w = min(__hip_atomic_load(&wk[cg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), 0xFFFFu);
+                        if (open) key = min(key, (w << 16) | (uint32_t)(u * kWave + lane));
                     }
+                    // wave minimum of the keys (fewest workers, then the lowest offset)
 #pragma unroll
-                    for (int u = 0; u < 4 && found < 0; ++u) {
-                        const uint64_t f = __ballot(open[u]);
-                        if (f) {
-                            uint32_t cg = start + k + (uint32_t)(u * kWave) + (uint32_t)__builtin_ctzll(f);
-                            if (cg >= (uint32_t)G) cg -= (uint32_t)G;
-                            found = (int)cg;
-                        }
+                    for (int d = 1; d < kWave; d <<= 1) key = min(key, (uint32_t)__shfl_xor((int)key, d, kWave));
+                    key = (uint32_t)uni((int)key);
+                    if (key != 0xFFFFFFFFu) {
+                        uint32_t cg = start + k + (key & 0xFFFFu);
+                        if (cg >= (uint32_t)G) cg -= (uint32_t)G;
+                        found = (int)cg;
                     }
                 }
                 if (found < 0) break;  // nothing left to claim anywhere (g < 0)
+                if (lane == 0) atomicAdd(&wk[found], 1u);
                 home = found;
             }
             if (lane == 0) {
@@ -1033,6 +1068,7 @@ static hipError_t launch_sample(const SampleShape &sh, int max_cdeg, int max_vde
             if ((e = hipMemsetAsync(ctl + 2, 0xFF, (size_t)4 * G, stream)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(ctl + 2 + G, 0, (size_t)4 * G, stream)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(ctl + 2 + 2 * G, 0xFF, (size_t)4 * G, stream)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(ctl + 2 + 3 * G, 0, (size_t)4 * G, stream)) != hipSuccess) return e;
             // graphs' home waves draw into check_lookup; pool rows: wave w uses variable_lookup row w
             hipLaunchKernelGGL(sk, dim3(W), dim3(kSeqT), lds, stream, sh, k0, k1, first_graph, G, check_lookup,
                                variable_lookup, ctl, max_attempts, bw, mdv);

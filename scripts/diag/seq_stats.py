@@ -29,7 +29,7 @@ _native.check(L.ldpc_sample_regular_dev(n, 3, 6, 5, G, G, chk.data_ptr(), var.da
 b.record(s)
 torch.cuda.synchronize()
 _native.check(L.ldpc_debug_seq_stats(st, 0), "stats")
-names = ["attempts", "aborted", "rounds", "kept", "lane_iters", "spread_iters", "coll_rounds", "val_fail"]
+names = ["attempts", "aborted", "rounds", "kept", "lane_iters", "spread_iters", "coll_rounds", "abort_rounds"]
 d = dict(zip(names, list(st)[:K]))
 emit = dict(zip(names, list(st)[K:]))
 ms = a.elapsed_time(b)
@@ -39,7 +39,8 @@ for k in names:
 R = max(d["rounds"], 1)
 A = max(d["attempts"], 1)
 print(f"  per graph: attempts {d['attempts'] / G:.1f}  rounds {d['rounds'] / G:.0f}  kept/round {d['kept'] / R:.1f}  "
-      f"rounds/attempt {d['rounds'] / A:.1f}")
+      f"rounds/attempt {d['rounds'] / A:.1f}  aborted/graph {d['aborted'] / G:.1f} (rounds before the abort "
+      f"{d['abort_rounds'] / max(d['aborted'], 1):.0f})")
 print(f"  per round: lane iters {d['lane_iters'] / R:.3f}  spread iters {d['spread_iters'] / R:.3f}  "
       f"collision rounds {d['coll_rounds'] / R:.3f}")
 print(f"  emit pass: attempts {emit['attempts']}  rounds {emit['rounds']}  kept/round {emit['kept'] / max(emit['rounds'], 1):.1f}")

@@ -37,6 +37,12 @@ for s in "$@"; do
     samp_stats)
         LDPC_LIB_PATH=build_variants/stats.so run 300 r06_samp_stats.log python scripts/diag/seq_stats.py ${N:-64800} ${G:-4096}
         rc=$? ;;
+    samp_stats16k)
+        LDPC_LIB_PATH=build_variants/stats.so run 300 r06_samp_stats16k.log python scripts/diag/seq_stats.py 64800 16384
+        rc=$? ;;
+    ens_time)
+        run 600 r06_ens_time.log bash -c "python scripts/diag/ens_time.py 0.42 16384 && python scripts/diag/ens_time.py 0.42 65536"
+        rc=$? ;;
     samp_prof)
         TAG=${TAG:-r06s} N=${N:-64800} G=${G:-4096} run 900 r06_samp_prof.log bash scripts/prof_sampler.sh
         rc=$? ;;
