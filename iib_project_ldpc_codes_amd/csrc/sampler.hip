@@ -157,6 +157,7 @@ constexpr int kSeqSlots = 2 * kSeqT;           // slots per round: two per lane
 constexpr int kSeqRing = 512;                  // ring: a round + the longest check it completes
 static_assert(kSeqSlots + kSeqMaxCdeg <= kSeqRing, "the ring must hold a round and the check it completes");
 static_assert(kSeqNW == 2, "the cut words hold two waves");
+static_assert(kSeqMaxE <= (1 << 19), "first-pass keys: an entry in 19 bits, the word index above bit 20");
 // LDS sync words of an attempt: reject flags by round parity, cut[parity][wave], claim broadcast
 enum { kSyFlag = 0, kSyCut = 2, kSyClaim = 8, kSeqSync = 16 };
 // LDS of an attempt: sy [kSeqSync] | tl [kSeqNW][2 kWave] | fin [kSeqFinal] | ring [kSeqRing] RT | bitmap [bw]
@@ -386,21 +387,44 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 for (int f = 0; f < kSeqFirstBlocks; ++f) cc[f] = blk | ((uint32_t)f << 20);
                 philox_blocks<kSeqFirstBlocks, kSeqPhiloxRounds>(cc, c1, g0, g1, K, Wf);
             }
+            // word j of a slot keys as (j << 20) | entry, all ones when the entry is used (the
+            // bitmap bit sign-extended by v_bfe_i32): the slot's pick is its lowest key.  Lemire's
+            // rejection (low product word below lt: probability R / 2^32 per word) is tested for
+            // the whole wave at once; only a wave holding such a word re-keys with the test.
+            constexpr int NWF = 2 * kSeqFirstBlocks;
             int i[2];
             bool act[2], need[2];
+            uint32_t key[2][NWF], low[2][NWF], mn[2];
+            uint32_t lmin = 0xFFFFFFFFu;
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const int x = base + 2 * tid + q;
                 act[q] = x >= x0 && x < xend;
-                int e[2 * kSeqFirstBlocks];
+                mn[q] = 0xFFFFFFFFu;
 #pragma unroll
-                for (int f = 0; f < kSeqFirstBlocks; ++f) {
-                    e[2 * f] = try_word(q ? Wf[f].y : Wf[f].x);
-                    e[2 * f + 1] = try_word(q ? Wf[f].w : Wf[f].z);
+                for (int j = 0; j < NWF; ++j) {
+                    const uint4 &W = Wf[j >> 1];
+                    const uint32_t w = (j & 1) ? (q ? W.w : W.z) : (q ? W.y : W.x);
+                    const uint64_t mm = (uint64_t)w * (uint32_t)R;
+                    const uint32_t e = (uint32_t)(mm >> 32);
+                    low[q][j] = (uint32_t)mm;
+                    const uint32_t used = (uint32_t)__builtin_amdgcn_sbfe((int)*bm_word(bmo, (int)e), e, 1u);
+                    key[q][j] = e | used | ((uint32_t)j << 20);
+                    mn[q] = min(mn[q], key[q][j]);
+                    lmin = min(lmin, low[q][j]);
                 }
-                i[q] = e[2 * kSeqFirstBlocks - 1];
+            }
+            if (__ballot(lmin < lt)) {  // rare: exact Lemire
 #pragma unroll
-                for (int j = 2 * kSeqFirstBlocks - 2; j >= 0; --j) i[q] = e[j] >= 0 ? e[j] : i[q];
+                for (int q = 0; q < 2; ++q) {
+                    mn[q] = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int j = 0; j < NWF; ++j) mn[q] = min(mn[q], low[q][j] < lt ? 0xFFFFFFFFu : key[q][j]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                i[q] = __builtin_amdgcn_sbfe((int)mn[q], 0u, 20u);  // the entry (< 2^19), or -1 (all ones)
                 need[q] = act[q] && i[q] < 0;
             }
             // later stages: the pool entries of the first draws are loaded now, so the global
