@@ -798,6 +798,7 @@ int ldpc_bp_decode_batch(const int32_t *variable_to_check_list, const int32_t *c
                          int dv, int dc, const float *llr, int B, int max_iters, int algo, float alpha,
                          int early_stop, float *post, uint8_t *hard, int32_t *its) {
     LDPC_REQUIRE((B == 0 || llr) && B >= 0, "bad soft batch arguments");
+    LDPC_REQUIRE(algo == LDPC_ALGO_SPA || algo == LDPC_ALGO_MINSUM, "algo must be LDPC_ALGO_SPA or LDPC_ALGO_MINSUM");
     ldpc_graph *g = nullptr;
     int rc = ldpc_graph_create(variable_to_check_list, check_to_variable_list, n, k, dv, dc, &g);
     if (rc) return rc;

@@ -3184,6 +3184,7 @@ hipError_t launch_bec_decode(const ldpc_graph &g, uint8_t *d_words, int B, int m
 }
 
 size_t bp_scratch_bytes(const ldpc_graph &g, int B, int iters, int algo, bool ep) {
+    algo = algo ? 1 : 0;  // as dispatch_bp_algo maps it: the slab decision must follow the path that runs
     // the per-workgroup posterior slabs only when the early-stop-with-posteriors decode will run
     // on bp_loc_kernel (choose_path may send it to bp_lds_kernel / bp_irr_kernel instead)
     const bool ep_slab = ep && g.loc_KP && choose_path(g, iters, true, false, algo, false) == BpPath::Loc;

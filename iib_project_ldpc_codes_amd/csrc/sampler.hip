@@ -126,9 +126,10 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
 //   * a round draws up to kSeqSlots (256) consecutive slots, two per lane (the pair of one Philox
 //     block: its words 0-1 are both slots' first two words), against the bitmap of the slots
 //     before the round; LDS atomic ORs mark the picks, and when two slots picked the same entry
-//     the round keeps the slots below the lowest slot that saw its bit already set (never fewer
-//     than the round's first slot, which is always right) -- a slot's result is its first draw
-//     not used by an earlier slot, so the later slots simply redraw next round from the updated
+//     the round keeps the slots below the second-lowest slot of the group of the lowest slot that
+//     saw its bit already set (found with the group's owner; at least the round's first slot,
+//     which is always right, and at most the exact cut) -- a slot's result is its first draw not
+//     used by an earlier slot, so the later slots simply redraw next round from the updated
 //     bitmap: exactly the sequential process, for any atomic order (tests/test_seq_sampler_rounds.py);
 //   * every check whose slots are all drawn is tested (variable ids kept in an LDS ring of the
 //     last kSeqRing slots); a repeat rejects the attempt (att+1).
@@ -159,7 +160,10 @@ static_assert(kSeqSlots + kSeqMaxCdeg <= kSeqRing, "the ring must hold a round a
 static_assert(kSeqNW == 2, "the cut words hold two waves");
 static_assert(kSeqMaxE <= (1 << 19), "first-pass keys: an entry in 19 bits, the word index above bit 20");
 // LDS sync words of an attempt: reject flags by round parity, cut[parity][wave], claim broadcast
-enum { kSyFlag = 0, kSyCut = 2, kSyClaim = 8, kSeqSync = 16 };
+// LDS sync words: reject flags by round parity [0, 2), per parity and wave the two lowest
+// colliding slots and the lowest one's pick [2, 14), the pick's owner per wave [14, 16), the
+// claim broadcast [16, 19)
+enum { kSyFlag = 0, kSyCut = 2, kSyOwn = 14, kSyClaim = 16, kSeqSync = 24 };
 // LDS of an attempt: sy [kSeqSync] | tl [kSeqNW][2 kWave] | fin [kSeqFinal] | ring [kSeqRing] RT | bitmap [bw]
 // (the bitmap last: its LDS address is a constant, folded into the ds instructions' offsets)
 constexpr uint32_t kSeqRingOff = 4u * (kSeqSync + 2 * kSeqT + kSeqFinal);
@@ -518,11 +522,21 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                 dup[q] = need[q] || (old & bit) != 0u;  // need: a slot without a word (over)
             }
             {
+                // this wave's two lowest colliding slots and the lowest one's pick (the cut below)
                 const uint64_t d0 = __ballot(dup[0]), d1 = __ballot(dup[1]);
-                int md = S;
-                if (d0) md = 2 * (wave * kWave + (int)__builtin_ctzll(d0));
-                if (d1) md = min(md, 2 * (wave * kWave + (int)__builtin_ctzll(d1)) + 1);
-                if (lane == 0) sy[kSyCut + 2 * par + wave] = md;
+                const uint64_t d0b = d0 & (d0 - 1), d1b = d1 & (d1 - 1);
+                const int la = d0 ? (int)__builtin_ctzll(d0) : 64, lb = d1 ? (int)__builtin_ctzll(d1) : 64;
+                const int ca = 2 * la, ca2 = d0b ? 2 * (int)__builtin_ctzll(d0b) : 128;  // slots 2 l + q of the wave
+                const int cb = 2 * lb + 1, cb2 = d1b ? 2 * (int)__builtin_ctzll(d1b) + 1 : 129;
+                const int m1 = min(ca, cb), m2 = ca < cb ? min(ca2, cb) : min(cb2, ca);
+                int e1 = -1;
+                if (m1 < 128) e1 = ca < cb ? __builtin_amdgcn_readlane(i[0], la) : __builtin_amdgcn_readlane(i[1], lb);
+                if (lane == 0) {
+                    int *cw = sy + kSyCut + 6 * par + 3 * wave;
+                    cw[0] = m1 < 128 ? wave * 2 * kWave + m1 : S;
+                    cw[1] = m2 < 128 ? wave * 2 * kWave + m2 : S;
+                    cw[2] = e1;
+                }
             }
             // ring: both slots of the pair in one store (base is even); a slot below x0 (x0 odd)
             // keeps its value, slots at or above the cut are redrawn (and rewritten) before any
@@ -538,16 +552,37 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             }
             seq_sync();  // (B) marks, cut words and ring
             const int tend = min(S, xend - base);
-            int t = min(uni(min(sy[kSyCut + 2 * par], sy[kSyCut + 2 * par + 1])), tend);
-            if (t < tend) {  // a collision: keep the slots below t (at least the first one)
+            const int *cw = sy + kSyCut + 6 * par;
+            const int a1 = uni(cw[0]), b1 = uni(cw[3]);
+            const int D = min(a1, b1);  // the lowest slot that found its bit set
+            int t = min(D, tend);
+            if (t < tend) {  // a collision
                 SEQ_STAT(PASS, kStCollRounds, 1);
-                t = max(t, x0 - base + 1);
+                // The round keeps the slots below the second-lowest slot of every group of equal
+                // picks.  D's group: if its owner (the slot that set the bit) is below D, D is
+                // that group's second-lowest and no other group's is lower -- t = D exactly;
+                // otherwise every group's second-lowest is at least min(owner, the next
+                // colliding slot d2) -- t = that (a slot of another group may be cut early: it
+                // redraws next round, the same result).  Never fewer than the round's first slot.
+                const int a2 = uni(cw[1]), b2 = uni(cw[4]);
+                const int d2 = a1 <= b1 ? min(a2, b1) : min(b2, a1);
+                const int eD = uni(a1 <= b1 ? cw[2] : cw[5]);
+                bool own[2];
+#pragma unroll
+                for (int q = 0; q < 2; ++q) own[q] = act[q] && !dup[q] && i[q] == eD;
+                const uint64_t o0 = __ballot(own[0]), o1 = __ballot(own[1]);
+                int om = S;
+                if (o0) om = 2 * (wave * kWave + (int)__builtin_ctzll(o0));
+                if (o1) om = min(om, 2 * (wave * kWave + (int)__builtin_ctzll(o1)) + 1);
+                if (lane == 0) sy[kSyOwn + wave] = om;
 #pragma unroll
                 for (int q = 0; q < 2; ++q)  // undo every pick of the round ...
                     if (act[q] && !dup[q])
                         __hip_atomic_fetch_and(bm_word(bmo, i[q]), ~(1u << (i[q] & 31)), __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
                 seq_sync();
+                const int oD = min(uni(sy[kSyOwn]), uni(sy[kSyOwn + 1]));
+                t = min(max(oD < D ? D : min(oD, d2), x0 - base + 1), tend);
 #pragma unroll
                 for (int q = 0; q < 2; ++q)  // ... and redo the kept ones
                     if (act[q] && !need[q] && 2 * tid + q < t)
@@ -598,7 +633,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
     };
 
     seq_clear_bm(bm, (R + 31) >> 5);
-    if (tid < 4) sy[tid] = tid < 2 ? 0 : S;
+    if (tid < 2) sy[kSyFlag + tid] = 0;
     __syncthreads();
     int cur = -1;  // offset of the current pool in `pools` (-1: stage 0, the sockets)
     while (R > kSeqFinal) {

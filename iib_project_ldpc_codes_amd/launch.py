@@ -79,7 +79,8 @@ def spawn_ranks(envs, argv, script=None, grace=5.0):
     procs = []
     rc = 0
     try:
-        procs = [subprocess.Popen([sys.executable, "-u", script] + list(argv), env=e) for e in envs]
+        for e in envs:  # appended one by one: a signal mid-spawn still reaps the ranks already started
+            procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=e))
         while procs:
             for p in list(procs):
                 c = p.poll()

@@ -2,8 +2,9 @@
 against the sequential definition it must equal (oracle/ldpc_oracle.c seq_attempt): up to 256
 slots (two per lane, two waves) drawn per round against the bitmap of the slots before the
 round, picks marked by atomic OR in an arbitrary order, and -- when slots picked the same pool
-entry -- only the slots below the lowest slot that found its bit already set kept (at least the
-round's first slot; undo every pick, redo the kept ones).  The word stream is a stand-in hash
+entry -- only the slots below the cut kept: D = the lowest slot that found its bit already set;
+t = D when its pick's owner (the slot that set the bit) is below it, else min(owner, the next
+such slot); at least the round's first slot (undo every pick, redo the kept ones).  The word stream is a stand-in hash
 (the rule, not Philox, is under test); pools compact at ceil(R/4) entries left, the last <= 64
 entries are shuffled.  CPU only."""
 import hashlib
@@ -87,9 +88,14 @@ def rounds(E, var, att, order_rng):
                 dup[s] = bm[cand[s]] == 1
                 bm[cand[s]] = 1
             tend = min(256, xend - base)
-            t = min([s for s in slots if dup[s]], default=tend)
+            dups = sorted(s for s in slots if dup[s])
+            t = min(dups[0], tend) if dups else tend
             if t < tend:
-                t = max(t, x0 - base + 1)  # the round's first slot is always right
+                D = dups[0]  # the lowest slot that found its bit set; its pick's owner set it
+                owner = min(s for s in slots if not dup[s] and cand[s] == cand[D])
+                d2 = dups[1] if len(dups) > 1 else 256
+                t = D if owner < D else min(owner, d2)
+                t = min(max(t, x0 - base + 1), tend)  # the round's first slot is always right
                 for s in slots:
                     if not dup[s]:
                         bm[cand[s]] = 0
