@@ -115,13 +115,13 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
 // drawn and the attempt stops there (a failing (3,6) attempt at n = 64,800 stops after ~1/5 of
 // the graph instead of paying a whole permutation):
 //   * slot x (in order) takes a uniform unused entry of the pool: its words -- word j = word
-//     2(j&1) + (x&1) of Philox ctr {x>>1 | (j>>1)<<20, tag|att<<2|3, g_lo, g_hi}, i.e. one block
+//     2(j&1) + (x&1) of Philox4x32-7 ctr {x>>1 | (j>>1)<<20, tag|att<<2|3, g_lo, g_hi}, i.e. one block
 //     holds words 2k, 2k+1 of the slot pair x>>1 -- give Lemire draws on [0, R) until one lands
 //     on an unused pool index (a bitmap in LDS); 1024 words without one reject the attempt
-//     (probability < (3/4)^1000);
-//   * the pool starts as all R = E sockets; when R' = ceil(R/4) entries are left the unused ones
+//     (probability < (1/2)^1000);
+//   * the pool starts as all R = E sockets; when R' = ceil(R/2) entries are left the unused ones
 //     are compacted in order into a new pool (global scratch, the variable_lookup row) with a
-//     fresh bitmap, so no draw ever sees more than 3/4 of its pool used; the last <= kSeqFinal
+//     fresh bitmap, so no draw ever sees more than half its pool used; the last <= kSeqFinal
 //     entries are Fisher-Yates-shuffled by one lane (stream {blk, tag|1<<30|att<<2|3, g});
 //   * a round draws up to kSeqSlots (256) consecutive slots, two per lane (the pair of one Philox
 //     block: its words 0-1 are both slots' first two words), against the bitmap of the slots
@@ -140,18 +140,12 @@ __device__ void sample_emit_var_side(const SampleShape &sh, const int32_t *chk, 
 // into the bitmap's LDS (fb = 0: global CAS, sample_emit_var_side).
 // oracle_sample_regular / oracle_sample_csr restate it bit for bit.
 constexpr int kSeqFinal = 64;
-#ifndef LDPC_SEQ_PHILOX_ROUNDS
-#define LDPC_SEQ_PHILOX_ROUNDS 10  // timing experiments only: the stream (and oracle) are Philox4x32-10
-#endif
-constexpr int kSeqPhiloxRounds = LDPC_SEQ_PHILOX_ROUNDS;
-#ifndef LDPC_SEQ_FIRST_BLOCKS
-#define LDPC_SEQ_FIRST_BLOCKS 2  // Philox blocks every slot pair draws up front (2 words per slot each)
-#endif
-constexpr int kSeqFirstBlocks = LDPC_SEQ_FIRST_BLOCKS;
-#ifndef LDPC_SEQ_SPLIT
-#define LDPC_SEQ_SPLIT 4  // a stage ends when ceil(R / LDPC_SEQ_SPLIT) pool entries are left
-#endif
-constexpr int kSeqSplit = LDPC_SEQ_SPLIT;
+// the draws' Philox4x32 rounds: 7, the crush-resistant minimum (Salmon et al., SC'11, Table 2;
+// 10 is Random123's default with a safety margin -- the channels keep 10, rocRAND's stream):
+// 28 VALU per block instead of 40, -5 % per graph
+constexpr int kSeqPhiloxRounds = 7;
+constexpr int kSeqFirstBlocks = 2;  // Philox blocks every slot pair draws up front (2 words per slot each)
+constexpr int kSeqSplit = 2;        // a stage ends when ceil(R / 2) pool entries are left (f <= 1/2)
 constexpr int kSeqNW = 2;                      // waves per attempt
 constexpr int kSeqT = kSeqNW * kWave;          // threads per attempt
 constexpr int kSeqSlots = 2 * kSeqT;           // slots per round: two per lane

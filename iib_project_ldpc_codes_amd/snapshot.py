@@ -28,10 +28,11 @@ VERSION = 1
 
 # The device sampler's graph stream (csrc/sampler.hip: which graph trial t gets): a resumed
 # ensemble run must draw its remaining graphs from the stream its first part drew from.
-# Round 6 changed the sequential-draw words (one Philox block = two words of a slot pair, was
-# one word of four slots): SAMPLER_RULE_R3 is the stream of rounds 3-5, and of the snapshots
-# written before the field existed (round 3) -- they no longer resume.
-SAMPLER_RULE = "one-level-rs<8192<=seq-draw-pair-words<=393216/philox4x32-10"
+# Round 6 changed the sequential-draw stream (one Philox4x32-7 block = two words of a slot pair,
+# was one Philox4x32-10 word of four slots; stages end at half the pool, was a quarter):
+# SAMPLER_RULE_R3 is the stream of rounds 3-5, and of the snapshots written before the field
+# existed (round 3) -- they no longer resume.
+SAMPLER_RULE = "one-level-rs/philox4x32-10<8192<=seq-draw-pair-words/philox4x32-7/split2<=393216"
 SAMPLER_RULE_R3 = "one-level-rs<8192<=seq-draw<=393216/philox4x32-10"
 
 

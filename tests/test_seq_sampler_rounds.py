@@ -5,7 +5,7 @@ round, picks marked by atomic OR in an arbitrary order, and -- when slots picked
 entry -- only the slots below the cut kept: D = the lowest slot that found its bit already set;
 t = D when its pick's owner (the slot that set the bit) is below it, else min(owner, the next
 such slot); at least the round's first slot (undo every pick, redo the kept ones).  The word stream is a stand-in hash
-(the rule, not Philox, is under test); pools compact at ceil(R/4) entries left, the last <= 64
+(the rule, not Philox, is under test); pools compact at ceil(R/2) entries left, the last <= 64
 entries are shuffled.  CPU only."""
 import hashlib
 import random
@@ -53,7 +53,7 @@ def _final(att, arr):
 def sequential(E, var, att):
     out, cur, R, x = [None] * E, list(var), E, 0
     while R > FINAL:
-        Rn = (R + 3) // 4
+        Rn = (R + 1) // 2
         used = [0] * R
         while x < E - Rn:
             i = _draw(att, x, R, used)
@@ -73,7 +73,7 @@ def rounds(E, var, att, order_rng):
     the picks of both waves are marked by atomic ORs in an arbitrary order."""
     out, cur, R, x0, nrounds = [None] * E, list(var), E, 0, 0
     while R > FINAL:
-        Rn = (R + 3) // 4
+        Rn = (R + 1) // 2
         xend = E - Rn
         bm = [0] * R
         while x0 < xend:
