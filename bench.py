@@ -11,11 +11,13 @@ Weak scaling: every rank decodes its own 65536-frame batch.
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Rank 0 prints one JSON line.  roofline: the decode kernel keeps every edge
-message in LDS, so its binding unit is on-chip: LDS cycles (per CU) or VALU
-issue cycles (per SIMD) per codeword-iteration from the committed HEAD issue
-model (ISSUE_PROFILE below, scripts/issue_model.py) x the live
+message in LDS, so its binding unit is on-chip: LDS-array cycles (per CU,
+PMC SQ_LDS_IDX_ACTIVE) or VALU-busy cycles (per SIMD, PMC SQ_ACTIVE_INST_VALU)
+per codeword-iteration, both measured by counters in the committed profile of
+this kernel (ISSUE_PROFILE below, scripts/issue_model.py), x the live
 codeword-iteration rate of the kernel (HIP events on the launch stream) over
-the unit's peak; the larger fraction is `roofline`.  roofline.hbm_model
+the unit's peak; the larger fraction is `roofline` (the issue model at the
+measured VALU prices rides beside it).  roofline.hbm_model
 keeps SURVEY.md 8(d)'s streaming byte model (2*E*4 + 2*n*4 = 320,000 B per
 codeword-iteration, above the HBM peak by design) beside the measured HBM
 traffic (PMC FETCH_SIZE/WRITE_SIZE).  cpu_baseline: the oracle's OpenMP fp32
@@ -241,25 +243,27 @@ def graph_cfg0():
     return TannerGraph.random_regular(1000, DV, DC, seed=1)
 
 
-ISSUE_PROFILE = os.path.join(ROOT, "profiles", "r05a_issue_model.json")
+ISSUE_PROFILE = os.path.join(ROOT, "profiles", "r06_issue_model.json")
 SIMDS, CUS, CLOCK_HZ = 1024, 256, 2.4e9
 
 
 def onchip_rooflines(cw_iters_per_s, kernel):
     """The units the LDS-resident kernel can saturate, per codeword-iteration, from the committed
-    HEAD issue model (ISSUE_PROFILE, scripts/issue_model.py: the kernel ISA's blocks x their
-    execution counts, cross-checked with and completed by the PMC counters of one launch):
-      valu: issue cycles per codeword-iteration at the MEASURED wave64 prices (plain f32 / integer
-            4.2, packed f32 5.3, transcendental 8.2; scripts/diag/valu_rate.hip,
-            profiles/r05_valu_rate*.jsonl) over 1024 SIMDs x 2.4 GHz; beside it the PMC
-            VALU-active fraction of the profiled launch (SQ_ACTIVE_INST_VALU counts 4 / 4 / 8);
+    issue model of this kernel (ISSUE_PROFILE, scripts/issue_model.py: its ISA blocks x their
+    execution counts, completed by the PMC counters of one profiled launch):
+      valu: VALU-busy cycles per codeword-iteration MEASURED by PMC SQ_ACTIVE_INST_VALU (x 4: one
+            quad-cycle per wave64 instruction, two per transcendental) over 1024 SIMDs x 2.4 GHz
+            -- the roofline's frac, a counter, not a price choice; beside it the issue model at
+            the chip-wide probe's prices (plain 4.2, packed f32 5.3, transcendental 8.2 cycles;
+            scripts/diag/valu_rate.hip) and the band those prices span: packed ops at 4.0 (what
+            the counter charges) .. 5.3 (distinct operand pairs) .. 7.5 (one register pair read
+            three times -- above 1.0 of peak with this mix, so not the headline's price);
       lds:  LDS-array cycles per codeword-iteration MEASURED by SQ_LDS_IDX_ACTIVE (every array
             cycle, bank conflicts included) over 256 CUs x 2.4 GHz; beside it the older transfer
-            model (MI355X_MICROARCH.md per-instruction costs -- a store's address + data transfer,
-            not its array cycles -- plus SQ_LDS_BANK_CONFLICT, which double-counts store conflicts
-            that hide under the transfer).
-    achieved = cycles x the live codeword-iteration rate of the kernel.  Returns (valu, lds), or
-    (None, None) when the committed model is of another kernel than the one that ran."""
+            model (MI355X_MICROARCH.md per-instruction costs plus SQ_LDS_BANK_CONFLICT).
+    achieved = cycles per codeword-iteration x the live codeword-iteration rate of this run's
+    kernel (HIP events).  Returns (valu, lds), or (None, None) when the committed model is of
+    another kernel than the one that ran."""
     if not os.path.exists(ISSUE_PROFILE):
         return None, None
     with open(ISSUE_PROFILE) as f:
@@ -267,35 +271,53 @@ def onchip_rooflines(cw_iters_per_s, kernel):
     if d.get("kernel_family") != kernel.split("<")[0]:  # the model describes another kernel: no roofline from it
         return None, None
     rel = os.path.relpath(ISSUE_PROFILE, ROOT)
-    v_cyc = d["valu_issue_cycles_per_codeword_iteration"]
-    valu = {"bound": "valu", "achieved": v_cyc * cw_iters_per_s / 1e9, "peak": SIMDS * CLOCK_HZ / 1e9,
-            "unit": "G SIMD-issue-cycles/s", "frac": v_cyc * cw_iters_per_s / (SIMDS * CLOCK_HZ),
-            "issue_cycles_per_codeword_iteration": v_cyc,
-            "wave_instr_per_codeword_iteration": d["wave_instr_per_codeword_iteration"],
-            "cycles_per_wave_instr": d["cycles"]["valu"], "prices": d.get("valu_prices"),
-            "profile": rel, "profile_git": d.get("git")}
-    alg = algorithmic_valu_cycles(d["cycles"]["valu"])
-    valu["algorithmic"] = {"issue_cycles_per_codeword_iteration": alg["cycles"],
-                           "frac": alg["cycles"] * cw_iters_per_s / (SIMDS * CLOCK_HZ), "definition": alg["definition"]}
+    peak = SIMDS * CLOCK_HZ
     pmc = d.get("pmc_per_codeword_iteration", {})
-    if "SQ_ACTIVE_INST_VALU" in pmc:  # VALU-active cycles per codeword-iteration (PMC, quad-cycles x 4)
-        valu["pmc_valu_active_frac"] = pmc["SQ_ACTIVE_INST_VALU"] * 4 * cw_iters_per_s / (SIMDS * CLOCK_HZ)
+    wi = d["wave_instr_per_codeword_iteration"]
+    prices = d["cycles"]["valu"]
+
+    def priced(packed):
+        return (wi["packed"] * packed + wi["plain"] * prices["plain"] + wi["trans"] * prices["trans"])
+
+    v_cyc = d["valu_issue_cycles_per_codeword_iteration"]
+    model = {"frac": v_cyc * cw_iters_per_s / peak, "issue_cycles_per_codeword_iteration": v_cyc,
+             "wave_instr_per_codeword_iteration": wi, "cycles_per_wave_instr": prices,
+             "price_band_frac": {f"packed_{pk:g}": priced(pk) * cw_iters_per_s / peak for pk in (4.0, 5.3, 7.5)},
+             "note": "packed price 4.0 = the counter's charge; 5.3 = chip-wide probe, distinct operand pairs; "
+                     "7.5 = probe with one register pair read three times (gives > 1.0 here: infeasible)"}
+    alg = algorithmic_valu_cycles(prices)
+    model["algorithmic"] = {"issue_cycles_per_codeword_iteration": alg["cycles"],
+                            "frac": alg["cycles"] * cw_iters_per_s / peak, "definition": alg["definition"]}
+    busy = pmc.get("SQ_ACTIVE_INST_VALU")
+    if busy:  # the measured VALU-busy cycles (quad-cycles x 4)
+        cyc = busy * 4
+        valu = {"bound": "valu", "achieved": cyc * cw_iters_per_s / 1e9, "peak": peak / 1e9,
+                "unit": "G SIMD-VALU-busy-cycles/s", "frac": cyc * cw_iters_per_s / peak,
+                "source": "PMC SQ_ACTIVE_INST_VALU x 4 per codeword-iteration (profiled launch of this kernel) "
+                          "x this run's live codeword-iteration rate",
+                "valu_busy_cycles_per_codeword_iteration": cyc,
+                "profiled_launch_valu_active_frac": d.get("profiled_valu_active_frac"),
+                "issue_model": model, "profile": rel, "profile_git": d.get("git")}
+    else:  # an older profile without the counter: the model
+        valu = dict(model, bound="valu", achieved=v_cyc * cw_iters_per_s / 1e9, peak=peak / 1e9,
+                    unit="G SIMD-issue-cycles/s", source="issue model (measured prices)", profile=rel,
+                    profile_git=d.get("git"))
     t_cyc = d["lds_cycles_per_codeword_iteration"]
     conf = d["lds_bank_conflict_cycles_per_codeword_iteration"]
-    model = {"frac": (t_cyc + conf) * cw_iters_per_s / (CUS * CLOCK_HZ),
-             "cycles_per_codeword_iteration": t_cyc + conf, "conflict_free_cycles": t_cyc,
-             "bank_conflict_cycles": conf, "cycles_per_wave_instr": d["cycles"]["lds"],
-             "lds_instr_per_codeword_iteration": d["lds_instr_per_codeword_iteration"]}
+    tmodel = {"frac": (t_cyc + conf) * cw_iters_per_s / (CUS * CLOCK_HZ),
+              "cycles_per_codeword_iteration": t_cyc + conf, "conflict_free_cycles": t_cyc,
+              "bank_conflict_cycles": conf, "cycles_per_wave_instr": d["cycles"]["lds"],
+              "lds_instr_per_codeword_iteration": d["lds_instr_per_codeword_iteration"]}
     idx = pmc.get("SQ_LDS_IDX_ACTIVE")
     if idx:
         lds = {"bound": "lds", "achieved": idx * cw_iters_per_s / 1e9, "peak": CUS * CLOCK_HZ / 1e9,
                "unit": "G LDS-array-cycles/s", "frac": idx * cw_iters_per_s / (CUS * CLOCK_HZ),
                "array_cycles_per_codeword_iteration": idx, "source": "PMC SQ_LDS_IDX_ACTIVE (measured)",
-               "transfer_model": model, "profile": rel, "profile_git": d.get("git")}
+               "transfer_model": tmodel, "profile": rel, "profile_git": d.get("git")}
     else:  # an older profile without the array counter: the model
         lds = {"bound": "lds", "achieved": (t_cyc + conf) * cw_iters_per_s / 1e9, "peak": CUS * CLOCK_HZ / 1e9,
-               "unit": "G LDS-cycles/s", "frac": model["frac"], "source": "transfer model + SQ_LDS_BANK_CONFLICT",
-               "transfer_model": model, "profile": rel, "profile_git": d.get("git")}
+               "unit": "G LDS-cycles/s", "frac": tmodel["frac"], "source": "transfer model + SQ_LDS_BANK_CONFLICT",
+               "transfer_model": tmodel, "profile": rel, "profile_git": d.get("git")}
     return valu, lds
 
 
@@ -320,7 +342,8 @@ def algorithmic_valu_cycles(prices=None):
 
 
 def load_traffic():
-    for name in ("r05a_pmc_traffic.json", "r04b_pmc_traffic.json", "r03a_pmc_traffic.json", "pmc_traffic.json"):
+    for name in ("r06_pmc_traffic.json", "r05a_pmc_traffic.json", "r04b_pmc_traffic.json", "r03a_pmc_traffic.json",
+                 "pmc_traffic.json"):
         p = os.path.join(ROOT, "profiles", name)
         if os.path.exists(p):
             with open(p) as f:

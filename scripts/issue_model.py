@@ -189,6 +189,8 @@ def main():
         "wave_executions": wx,
         "pmc_per_codeword_iteration": {k: v / units for k, v in d.items() if k.startswith("SQ_")},
     }
+    if "GRBM_GUI_ACTIVE" in d and "SQ_ACTIVE_INST_VALU" in d:  # the profiled launch's own VALU-busy fraction
+        out["profiled_valu_active_frac"] = d["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * d["GRBM_GUI_ACTIVE"] / 8)
     json.dump(out, open(out_path, "w"), indent=1)
     print(json.dumps(out, indent=1))
 

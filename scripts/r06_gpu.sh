@@ -8,6 +8,7 @@
 #   samp_stats   search-pass counters of a -DLDPC_SEQ_STATS=1 build (build_variants/stats.so)
 #   samp_prof    rocprofv3 kernel trace + PMC passes of one sampler launch (scripts/prof_sampler.sh)
 #   dropin       drop-in message_passing tests + per-call rates (bench.dropin_*_rates)
+#   hprof        headline decode: rocprofv3 trace of the bench command + PMC passes (scripts/profile.sh)
 #   gputests     the whole -m gpu suite
 #   bench        bench.py (default arguments)
 set -u
@@ -53,6 +54,15 @@ for s in "$@"; do
             run 300 r06_dropin_time.log python -c "import json, bench; print(json.dumps({'gpu': bench.dropin_gpu_rates(2.0), 'ref': bench.dropin_reference_rates(2.0)}, indent=1))"
             rc=$?
         fi ;;
+    hprof)
+        PMC_GROUPS="FETCH_SIZE
+WRITE_SIZE
+SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS
+SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT
+SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_SALU
+SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_BRANCH" \
+        TAG=${HTAG:-r06h} KREGEX=bp_loc run 900 r06_hprof.log bash scripts/profile.sh
+        rc=$? ;;
     gputests)
         run 1500 r06_gputests.log $PYT tests -m gpu
         rc=$? ;;
