@@ -434,12 +434,12 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             }
             const bool firstok0 = !need[0], firstok1 = !need[1];
             // retries, within the wave: while many slots still look every lane draws the next
-            // block of its own pair; once at most 32 do, the wave spreads them -- L = 2..16 lanes
+            // block of its own pair; once at most 16 do, the wave spreads them -- L = 4..16 lanes
             // per slot, each trying one of the slot's next L words, the lowest passing word wins
             // (a slot's words are tried in order, so the result is the same)
             uint32_t j0 = 2 * kSeqFirstBlocks;  // next word index of every slot still looking (even)
             bool over = false;
-            for (;;) {
+            for (bool any = __ballot(need[0] || need[1]) != 0ull; any;) {  // (uniform; most rounds: none)
                 const uint64_t mq0 = __ballot(need[0]), mq1 = __ballot(need[1]);
                 const int C = __popcll(mq0) + __popcll(mq1);
                 if (C == 0) break;
@@ -447,7 +447,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                     over = true;
                     break;
                 }
-                if (C > 32) {
+                if (C > 16) {  // (spreading would give each slot at most two lanes: the same words, more work)
                     SEQ_STAT(PASS, kStLaneIters, 1);
                     const uint4 W = philox_block<kSeqPhiloxRounds>(blk | (j0 << 19), c1, g0, g1, K);  // (j0 >> 1) << 20
 #pragma unroll
@@ -518,17 +518,21 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             {
                 // this wave's two lowest colliding slots and the lowest one's pick (the cut below)
                 const uint64_t d0 = __ballot(dup[0]), d1 = __ballot(dup[1]);
-                const uint64_t d0b = d0 & (d0 - 1), d1b = d1 & (d1 - 1);
-                const int la = d0 ? (int)__builtin_ctzll(d0) : 64, lb = d1 ? (int)__builtin_ctzll(d1) : 64;
-                const int ca = 2 * la, ca2 = d0b ? 2 * (int)__builtin_ctzll(d0b) : 128;  // slots 2 l + q of the wave
-                const int cb = 2 * lb + 1, cb2 = d1b ? 2 * (int)__builtin_ctzll(d1b) + 1 : 129;
-                const int m1 = min(ca, cb), m2 = ca < cb ? min(ca2, cb) : min(cb2, ca);
-                int e1 = -1;
-                if (m1 < 128) e1 = ca < cb ? __builtin_amdgcn_readlane(i[0], la) : __builtin_amdgcn_readlane(i[1], lb);
+                int c1 = S, c2 = S, e1 = -1;
+                if (d0 | d1) {  // (uniform; most rounds have no collision)
+                    const uint64_t d0b = d0 & (d0 - 1), d1b = d1 & (d1 - 1);
+                    const int la = d0 ? (int)__builtin_ctzll(d0) : 64, lb = d1 ? (int)__builtin_ctzll(d1) : 64;
+                    const int ca = 2 * la, ca2 = d0b ? 2 * (int)__builtin_ctzll(d0b) : 128;  // slots 2 l + q of the wave
+                    const int cb = 2 * lb + 1, cb2 = d1b ? 2 * (int)__builtin_ctzll(d1b) + 1 : 129;
+                    const int m1 = min(ca, cb), m2 = ca < cb ? min(ca2, cb) : min(cb2, ca);
+                    e1 = ca < cb ? __builtin_amdgcn_readlane(i[0], la) : __builtin_amdgcn_readlane(i[1], lb);
+                    c1 = wave * 2 * kWave + m1;
+                    c2 = m2 < 128 ? wave * 2 * kWave + m2 : S;
+                }
                 if (lane == 0) {
                     int *cw = sy + kSyCut + 6 * par + 3 * wave;
-                    cw[0] = m1 < 128 ? wave * 2 * kWave + m1 : S;
-                    cw[1] = m2 < 128 ? wave * 2 * kWave + m2 : S;
+                    cw[0] = c1;
+                    cw[1] = c2;
                     cw[2] = e1;
                 }
             }

@@ -6,7 +6,8 @@
 // Grid: 256 x W workgroups of 256 threads (one wave per SIMD per workgroup, so W waves per
 // SIMD when the dispatcher spreads them), every lane runs CHAINS independent chains of one
 // instruction REPS times.  Per-SIMD cycles per wave-instruction =
-//     event_time * clock * 1024 SIMDs / (wave-instructions issued),
+//     (event_time(REPS) - event_time(REPS / 2)) * clock * 1024 SIMDs / (wave-instructions of the
+//     difference)  -- the differential cancels launch ramp-up, tail and fixed per-wave work,
 // quoted at the nominal 2.4 GHz and at the in-kernel clock (delta s_memtime / delta
 // s_memrealtime x 100 MHz, median over workgroups).  A one-workgroup run (the old probe's
 // shape) reports the same two clocks, which shows what its s_memtime cycles were.
@@ -71,54 +72,71 @@ __global__ __launch_bounds__(256) void kern(uint32_t *out, uint64_t *stamp, uint
     }
 }
 
+// instructions a step issues per chain (OP 10: a packed FMA and a plain add)
+template <int OP> constexpr int instr_per_step() { return OP == 10 ? 2 : 1; }
+
+// One timed series: 5 launches of `reps` repetitions after 3 warm-up launches; returns the event
+// milliseconds of the 5 and fills the stamps of the last.
+template <int OP>
+float timed(uint32_t *out, uint64_t *stamp, int blocks, int reps) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    for (int w = 0; w < 3; ++w) kern<OP><<<blocks, 256>>>(out, stamp, 1 + w, reps);  // warm the clock
+    hipDeviceSynchronize();
+    hipEventRecord(a);
+    for (int l = 0; l < 5; ++l) kern<OP><<<blocks, 256>>>(out, stamp, 7 + l, reps);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return ms;
+}
+
+// Differential: the series at reps and at reps / 2, so launch ramp-up, tail and fixed per-wave
+// cost cancel; wave-instructions = blocks x 4 waves x (reps - reps/2) x 4 unroll x CHAINS x
+// instructions per step.
 template <int OP>
 void run(const char *name, int blocks, int reps, bool one_wg) {
     uint32_t *out;
     uint64_t *stamp;
     hipMalloc(&out, (size_t)4 * 256 * blocks);
     hipMalloc(&stamp, (size_t)16 * blocks);
-    hipEvent_t a, b;
-    hipEventCreate(&a);
-    hipEventCreate(&b);
-    for (int w = 0; w < 3; ++w) kern<OP><<<blocks, 256>>>(out, stamp, 1 + w, reps);  // warm the clock
-    hipDeviceSynchronize();
-    const int launches = 5;
-    hipEventRecord(a);
-    for (int l = 0; l < launches; ++l) kern<OP><<<blocks, 256>>>(out, stamp, 7 + l, reps);
-    hipEventRecord(b);
-    hipEventSynchronize(b);
-    float ms = 0;
-    hipEventElapsedTime(&ms, a, b);
+    const int half = reps / 2;
+    const float ms_half = timed<OP>(out, stamp, blocks, half);
+    std::vector<uint64_t> hh((size_t)2 * blocks);
+    hipMemcpy(hh.data(), stamp, (size_t)16 * blocks, hipMemcpyDeviceToHost);
+    const float ms = timed<OP>(out, stamp, blocks, reps);
     std::vector<uint64_t> h((size_t)2 * blocks);
     hipMemcpy(h.data(), stamp, (size_t)16 * blocks, hipMemcpyDeviceToHost);
-    std::vector<double> clk(blocks), cyc(blocks);
+    std::vector<double> clk(blocks), dcyc(blocks);
     for (int i = 0; i < blocks; ++i) {
         clk[i] = (double)h[2 * i] / (double)h[2 * i + 1] * 0.1;  // GHz: memtime ticks per 100 MHz tick
-        cyc[i] = (double)h[2 * i];
+        dcyc[i] = (double)h[2 * i] - (double)hh[2 * i];
     }
     std::sort(clk.begin(), clk.end());
-    std::sort(cyc.begin(), cyc.end());
+    std::sort(dcyc.begin(), dcyc.end());
     const double ghz = clk[blocks / 2];
-    const double wave_instr = (double)blocks * 4 * reps * 4 * CHAINS;  // 4 waves per workgroup
-    const double s = ms * 1e-3;
+    const double per_wave = (double)(reps - half) * 4 * CHAINS * instr_per_step<OP>();  // per wave, differential
+    const double ds = (ms - ms_half) * 1e-3 / 5;  // seconds per launch, differential
     if (one_wg) {
         // one workgroup = one wave per SIMD on one CU: cycles per wave-instruction of ONE wave
-        const double per_memtime = cyc[blocks / 2] / ((double)reps * 4 * CHAINS);
         printf("{\"op\": \"%s\", \"shape\": \"1 workgroup, 1 wave/SIMD\", \"memtime_ghz\": %.3f, "
                "\"memtime_cycles_per_wave_instr\": %.3f, \"event_cycles_per_wave_instr_at_2.4GHz\": %.3f}\n",
-               name, ghz, per_memtime, s / launches * 2.4e9 / ((double)reps * 4 * CHAINS));
+               name, ghz, dcyc[blocks / 2] / per_wave, ds * 2.4e9 / per_wave);
     } else {
         const int W = blocks / 256;
+        const double wave_instr = (double)blocks * 4 * per_wave;
         printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"ms_per_launch\": %.4f, \"memtime_ghz\": %.3f, "
-               "\"simd_cycles_per_wave_instr_at_2.4GHz\": %.3f, \"simd_cycles_per_wave_instr_at_memtime_clock\": %.3f}\n",
-               name, W, ms / launches, ghz, s * 2.4e9 * 1024 / (wave_instr * launches),
-               s * ghz * 1e9 * 1024 / (wave_instr * launches));
+               "\"simd_cycles_per_wave_instr_at_2.4GHz\": %.3f, \"simd_cycles_per_wave_instr_at_memtime_clock\": %.3f, "
+               "\"method\": \"differential: (t(reps) - t(reps/2)), 5 launches each\"}\n",
+               name, W, ms / 5, ghz, ds * 2.4e9 * 1024 / wave_instr, ds * ghz * 1e9 * 1024 / wave_instr);
     }
     fflush(stdout);
     hipFree(out);
     hipFree(stamp);
-    hipEventDestroy(a);
-    hipEventDestroy(b);
 }
 
 template <int OP>

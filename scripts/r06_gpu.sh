@@ -9,6 +9,7 @@
 #   samp_prof    rocprofv3 kernel trace + PMC passes of one sampler launch (scripts/prof_sampler.sh)
 #   dropin       drop-in message_passing tests + per-call rates (bench.dropin_*_rates)
 #   hprof        headline decode: rocprofv3 trace of the bench command + PMC passes (scripts/profile.sh)
+#   valu         VALU issue-price probe (build_diag/valu_rate, scripts/diag/valu_rate.hip)
 #   gputests     the whole -m gpu suite
 #   bench        bench.py (default arguments)
 set -u
@@ -62,6 +63,9 @@ SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACT
 SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_SALU
 SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_BRANCH" \
         TAG=${HTAG:-r06h} KREGEX=bp_loc run 900 r06_hprof.log bash scripts/profile.sh
+        rc=$? ;;
+    valu)
+        run 300 r06_valu_rate.jsonl ./build_diag/valu_rate
         rc=$? ;;
     gputests)
         run 1500 r06_gputests.log $PYT tests -m gpu
