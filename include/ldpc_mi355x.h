@@ -54,6 +54,10 @@ extern "C" {
  * semantics: Mvc (0/1/2, int32[n]) decoded in place, errors[it] += erasure
  * count per iteration (caller zeroes it), stall skip, returns the break
  * iteration or `iterations`.  Runs one codeword on the current HIP device.
+ * Per call: the lists are compared with the last call's (exact memcmp) and the
+ * cached device graph reused, or refilled in place for a new code of the same
+ * shape; the word and errors[] travel through pinned staging, one copy each
+ * way, one stream synchronisation (thread-safe; one cache per process).
  */
 int message_passing(int *Mvc, int iterations, int *variable_to_check_list,
                     int *check_to_variable_list, int *errors, int n, int k, int dv, int dc);
