@@ -145,10 +145,7 @@ constexpr int kSeqFinal = 64;
 // 28 VALU per block instead of 40, -5 % per graph
 constexpr int kSeqPhiloxRounds = 7;
 constexpr int kSeqFirstBlocks = 2;  // Philox blocks every slot pair draws up front (2 words per slot each)
-constexpr int kSeqSplit = 2;
-#ifndef LDPC_SEQ_PRIO
-#define LDPC_SEQ_PRIO 0  // timing experiments: wave priority 1 for the mark phase (1) / the validation (2)
-#endif        // a stage ends when ceil(R / 2) pool entries are left (f <= 1/2)
+constexpr int kSeqSplit = 2;        // a stage ends when ceil(R / 2) pool entries are left (f <= 1/2)
 constexpr int kSeqNW = 2;                      // waves per attempt
 constexpr int kSeqT = kSeqNW * kWave;          // threads per attempt
 constexpr int kSeqSlots = 2 * kSeqT;           // slots per round: two per lane
@@ -506,7 +503,6 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             }
             if (over && lane == 0) sy[kSyFlag + par] = 1;
             seq_sync();  // (A) every wave's draws read the bitmap of the slots before the round
-            if (LDPC_SEQ_PRIO == 1) __builtin_amdgcn_s_setprio(1);
             if (uni(sy[kSyFlag + (par ^ 1)])) return false;  // the previous round rejected the attempt
             // mark the picks; a pick whose bit was already set (by another slot of the round)
             // is a collision, and the round keeps the slots below the lowest such slot
@@ -553,7 +549,6 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
                     *reinterpret_cast<int2 *>(ring + p) = make_int2(v0, val[1]);
             }
             seq_sync();  // (B) marks, cut words and ring
-            if (LDPC_SEQ_PRIO == 1) __builtin_amdgcn_s_setprio(0);
             const int tend = min(S, xend - base);
             const int *cw = sy + kSyCut + 6 * par;
             const int a1 = uni(cw[0]), b1 = uni(cw[3]);
@@ -604,9 +599,7 @@ __device__ bool seq_attempt(const SeqCtx &c, int att, int32_t *out, int32_t *poo
             }
             SEQ_STAT(PASS, kStKept, base + t - x0);
             x0 = base + t;
-            if (LDPC_SEQ_PRIO == 2) __builtin_amdgcn_s_setprio(1);
             validate(x0);
-            if (LDPC_SEQ_PRIO == 2) __builtin_amdgcn_s_setprio(0);
             par ^= 1;
         }
         return true;
