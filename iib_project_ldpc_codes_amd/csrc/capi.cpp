@@ -790,7 +790,7 @@ int ldpc_bp_decode_batch_dev(const ldpc_graph *g, const float *d_llr, int B, int
         scratch = static_cast<float *>(ws.scratch.p);
     }
     LDPC_HIP(launch_bp_decode(*g, d_llr, B, max_iters, algo, alpha, early_stop, d_post, d_hard, d_its,
-                              static_cast<hipStream_t>(stream), scratch));
+                              static_cast<hipStream_t>(stream), scratch, sb));
     return LDPC_OK;
 }
 
@@ -830,7 +830,7 @@ int ldpc_bp_decode_batch(const int32_t *variable_to_check_list, const int32_t *c
         if (B > 0) {
             // no posteriors asked for: early stop may take the hard-decision path (bp_loc_kernel)
             e = launch_bp_decode(*g, dl, B, max_iters, algo, alpha, early_stop, post ? dp : nullptr, dh, di, nullptr,
-                                 static_cast<float *>(ws.scratch.p));
+                                 static_cast<float *>(ws.scratch.p), ws.scratch.cap);
             if (e == hipSuccess) e = hipDeviceSynchronize();
             if (e == hipSuccess && post) e = hipMemcpy(post, dp, nb * 4, hipMemcpyDeviceToHost);
             if (e == hipSuccess && hard) e = hipMemcpy(hard, dh, nb, hipMemcpyDeviceToHost);
@@ -892,16 +892,18 @@ int ldpc_mc_batch_dev(const ldpc_graph *g, int channel, float param, uint64_t se
     LDPC_HIP(ws.its.ensure(sizeof(int32_t) * (size_t)B));
     LDPC_HIP(ws.cutoff.ensure(16));
     float *scratch = nullptr;
+    size_t sbytes = 0;
     if (channel != LDPC_CH_BEC) {
         const size_t sb = bp_scratch_bytes(*g, B, max_iters, algo, false);
         if (sb) {
             LDPC_HIP(ws.scratch.ensure(sb));
             scratch = static_cast<float *>(ws.scratch.p);
+            sbytes = ws.scratch.cap;
         }
     }
     int32_t *trial = static_cast<int32_t *>(ws.trial.p), *its = static_cast<int32_t *>(ws.its.p);
     LDPC_HIP(launch_mc_decode(*g, channel, p, p2, seed, first_cw, B, max_iters, algo, alpha, early_stop, trial, its,
-                              s, scratch));
+                              s, scratch, sbytes));
     LDPC_HIP(launch_mc_reduce(trial, its, B, max_iters, expurgation, stop_frame_errors, d_counters,
                               static_cast<int32_t *>(ws.cutoff.p), s));
     return LDPC_OK;
@@ -1203,7 +1205,7 @@ int ldpc_mc_ml_batch_dev(const ldpc_graph *g, int n, int dv, int dc, float eps, 
             LDPC_HIP(launch_mc_bec_ensemble(n, dv, dc, chk, var, p, seed, first_cw, B, max_iters, trial, its, s));
         else
             LDPC_HIP(launch_mc_decode(*g, LDPC_CH_BEC, p, p2, seed, first_cw, B, max_iters, 0, 1.0f, 0, trial, its,
-                                      s, nullptr));
+                                      s, nullptr, 0));
         // the stop rule counts message-passing frame errors (parallel_simulator.py:226-231)
         LDPC_HIP(launch_mc_reduce(trial, its, B, max_iters, expurgation, stop_frame_errors, d_counters_mp, cut, s));
         LDPC_HIP(launch_mc_reduce_cut(du, nullptr, B, 0, -1, cut, d_counters_ml, s));

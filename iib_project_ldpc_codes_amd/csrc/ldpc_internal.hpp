@@ -152,12 +152,15 @@ hipError_t launch_bec_decode(const ldpc_graph &g, uint8_t *d_words, int B, int m
 
 hipError_t launch_bp_decode(const ldpc_graph &g, const float *d_llr, int B, int max_iters, int algo,
                             float alpha, int early_stop, float *d_post, uint8_t *d_hard,
-                            int32_t *d_its, hipStream_t stream, float *d_scratch);
+                            int32_t *d_its, hipStream_t stream, float *d_scratch, size_t scratch_bytes);
 
 // Bytes of global scratch launch_bp_decode / launch_mc_decode need for this graph/batch (0
 // when the messages fit in LDS); ep_slab: an early-stop decode that returns posteriors (the
 // local-edge kernel's per-workgroup slabs; no other mode uses them).
-// ep: an early-stop decode that returns posteriors (the slabs are sized only if it runs on bp_loc_kernel)
+// ep: an early-stop decode that returns posteriors (the slabs are sized only if it runs on bp_loc_kernel).
+// The launchers check the layout of the path that runs against scratch_bytes and refuse
+// (hipErrorInvalidValue) one that would not fit, so a sizing rule that drifts from the dispatch
+// fails loudly instead of writing past the buffer.
 size_t bp_scratch_bytes(const ldpc_graph &g, int B, int iters, int algo, bool ep);
 
 hipError_t launch_channel(int channel, float p, float p2, uint64_t seed, uint64_t first_cw, int n,
@@ -168,7 +171,7 @@ hipError_t launch_channel(int channel, float p, float p2, uint64_t seed, uint64_
 hipError_t launch_mc_decode(const ldpc_graph &g, int channel, float p, float p2, uint64_t seed,
                             uint64_t first_cw, int B, int max_iters, int algo, float alpha,
                             int early_stop, int32_t *trial, int32_t *trial_its, hipStream_t stream,
-                            float *d_scratch);
+                            float *d_scratch, size_t scratch_bytes);
 hipError_t launch_mc_reduce(const int32_t *trial, const int32_t *trial_its, int B, int max_iters,
                             int expurgation, int64_t stop_frame_errors, int64_t *d_counters,
                             int32_t *d_cutoff, hipStream_t stream);

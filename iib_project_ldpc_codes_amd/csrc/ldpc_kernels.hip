@@ -806,6 +806,7 @@ struct BpArgs {
     int32_t *trial;  // [B][max_iters+1]
     // generic kernel, messages in global scratch
     float *scratch;
+    size_t scratch_bytes;  // (host) bytes at scratch: the launchers refuse a layout needing more
     // LDS kernel lane layout (ldpc_graph::lane_var / lane_slot)
     const int32_t *lane_var, *lane_slot;
     int lds_slots;  // generic GMEM kernel: message slots [0, lds_slots) kept in LDS
@@ -3014,6 +3015,10 @@ hipError_t launch_generic(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     auto k = bp_generic_kernel<T, MAXDC, ALGO, ET, MC, GMEM>;
     size_t lds = GMEM ? (MC ? (((size_t)(a.max_iters + 1) * 4 + 15) & ~(size_t)15) : 0)
                       : generic_lds_bytes(g, a.max_iters, MC);
+    int grid = a.B;
+    if (GMEM) grid = a.B < LDPC_GMEM_GRID ? a.B : LDPC_GMEM_GRID;
+    if (GMEM && (!a.scratch || a.scratch_bytes < (((size_t)g.E * 5 + (size_t)g.n * 4 + 15) & ~(size_t)15) * (size_t)grid))
+        return hipErrorInvalidValue;
     if (GMEM) {  // fill the rest of the CU's LDS with the first message slots
         const size_t room = kLdsMax - 4096 - lds;
         a.lds_slots = LDPC_GMEM_HYB ? (int)std::min<size_t>((size_t)g.E, room / 4) : 0;
@@ -3021,8 +3026,6 @@ hipError_t launch_generic(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     }
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
-    int grid = a.B;
-    if (GMEM) grid = a.B < LDPC_GMEM_GRID ? a.B : LDPC_GMEM_GRID;
     hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, s, a);
     return hipGetLastError();
 }
@@ -3035,7 +3038,7 @@ hipError_t launch_loc_shape(const ldpc_graph &g, BpArgs a, hipStream_t s) {
             auto k = bp_loc_kernel<DLO, DHI, D0, D1, KP, T, ALGO, A0, A1, true, false, true>;
             hipError_t e = allow_lds(k, lds);
             if (e != hipSuccess) return e;
-            if (!a.scratch) return hipErrorInvalidValue;
+            if (!a.scratch || a.scratch_bytes < loc_ep_slab_floats(g) * 4 + sizeof(uint32_t)) return hipErrorInvalidValue;
             const unsigned grid = (unsigned)std::min<int>(a.B, loc_ep_grid());
             a.work = reinterpret_cast<uint32_t *>(a.scratch + loc_ep_slab_floats(g));
             e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), s);
@@ -3048,7 +3051,8 @@ hipError_t launch_loc_shape(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     hipError_t e = allow_lds(k, lds);
     if (e != hipSuccess) return e;
     unsigned grid = (unsigned)a.B;
-    if ((ET || LDPC_LOC_PERSIST > 1) && LDPC_LOC_PERSIST && a.scratch) {  // persistent grid on a codeword counter
+    if ((ET || LDPC_LOC_PERSIST > 1) && LDPC_LOC_PERSIST && a.scratch &&
+        a.scratch_bytes >= sizeof(uint32_t)) {  // persistent grid on a codeword counter
         grid = (unsigned)std::min<int>(a.B, loc_ep_grid());
         a.work = reinterpret_cast<uint32_t *>(a.scratch);
         if ((e = hipMemsetAsync(a.work, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
@@ -3111,7 +3115,8 @@ hipError_t launch_irr(const ldpc_graph &g, BpArgs a, hipStream_t s) {
     a.irr_KC = g.irr_KC;
     a.irr_S = g.irr_S;
     a.irr_P = g.irr_P;
-    if (irr_slab(g) && !a.scratch) return hipErrorInvalidValue;
+    if (irr_slab(g) && (!a.scratch || a.scratch_bytes < (size_t)g.irr_P * 4 * (size_t)std::min(a.B, LDPC_GMEM_GRID)))
+        return hipErrorInvalidValue;
 #define IRR_CASE(DC, VPT) \
     if (g.irr_DC == DC && g.irr_VPT == VPT) return launch_irr_shape<DC, VPT, ALGO, ET, MC>(g, a, s);
     IRR_CASE(6, 5) IRR_CASE(6, 10) IRR_CASE(6, 20) IRR_CASE(8, 5) IRR_CASE(8, 10) IRR_CASE(8, 20)
@@ -3218,7 +3223,7 @@ const char *bp_kernel_name(const ldpc_graph &g, int early_stop) {
 
 hipError_t launch_bp_decode(const ldpc_graph &g, const float *d_llr, int B, int max_iters, int algo,
                             float alpha, int early_stop, float *d_post, uint8_t *d_hard,
-                            int32_t *d_its, hipStream_t stream, float *d_scratch) {
+                            int32_t *d_its, hipStream_t stream, float *d_scratch, size_t scratch_bytes) {
     if (B <= 0) return hipSuccess;
     BpArgs a = bp_args(g, B, max_iters, alpha);
     a.llr = d_llr;
@@ -3226,6 +3231,7 @@ hipError_t launch_bp_decode(const ldpc_graph &g, const float *d_llr, int B, int 
     a.hard = d_hard;
     a.its = d_its;
     a.scratch = d_scratch;
+    a.scratch_bytes = d_scratch ? scratch_bytes : 0;
     return dispatch_bp_algo<false>(g, a, algo, early_stop, stream);
 }
 
@@ -3241,7 +3247,8 @@ hipError_t launch_channel(int channel, float p, float p2, uint64_t seed, uint64_
 
 hipError_t launch_mc_decode(const ldpc_graph &g, int channel, float p, float p2, uint64_t seed,
                             uint64_t first_cw, int B, int max_iters, int algo, float alpha, int early_stop,
-                            int32_t *trial, int32_t *trial_its, hipStream_t stream, float *d_scratch) {
+                            int32_t *trial, int32_t *trial_its, hipStream_t stream, float *d_scratch,
+                            size_t scratch_bytes) {
     if (B <= 0) return hipSuccess;
     if (channel == 0) {
         BecArgs a = bec_args(g);
@@ -3270,6 +3277,7 @@ hipError_t launch_mc_decode(const ldpc_graph &g, int channel, float p, float p2,
     a.trial = trial;
     a.its = trial_its;
     a.scratch = d_scratch;
+    a.scratch_bytes = d_scratch ? scratch_bytes : 0;
     return dispatch_bp_algo<true>(g, a, algo, early_stop, stream);
 }
 

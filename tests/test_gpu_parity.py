@@ -303,6 +303,32 @@ def test_minsum_bit_exact(torch, irregular, early_stop):
 
 
 @pytest.mark.parametrize("irregular", [False, True])
+def test_early_stop_posteriors_more_frames_than_slabs(torch, irregular):
+    """Early stop with posteriors on more frames than the persistent grids hold slabs for
+    (B = 1,100 > 2 x 256 workgroups): the regular code runs bp_loc_kernel's slab path, the
+    irregular one (min-sum early stop needs one check class there) falls back to another
+    kernel.  The launchers refuse a scratch smaller than the path's layout, so a slab sizing
+    that drifted from the dispatch fails here instead of writing past the buffer.  Min-sum:
+    bit-exact against the oracle."""
+    from iib_project_ldpc_codes_amd import decoder, ensembles
+    from iib_project_ldpc_codes_amd.graph import TannerGraph
+    B = 1100
+    if irregular:
+        g = ensembles.sample_irregular(ensembles.RSU_DL4, 4000, seed=3, deg2="zigzag")
+    else:
+        g = TannerGraph.random_regular(1000, 3, 6, seed=14)
+    csr = g.to_csr()
+    llr = oracle.channel(oracle.CH_AWGN, 0.80, 15, 0, g.n, B)
+    for algo, code, alpha in (("minsum", 1, 0.75), ("spa", 0, 1.0)):
+        post, hard, its = decoder.bp_decode(g, llr, 30, algo, alpha=alpha, early_stop=True)
+        opost, ohard, oits = oracle.bp_decode_batch(csr, llr, 30, code, alpha=alpha, early_stop=True)
+        if code == 1:
+            np.testing.assert_array_equal(post, opost)
+            np.testing.assert_array_equal(its, oits)
+        assert np.mean(np.all(hard == ohard, axis=1)) >= 0.98
+
+
+@pytest.mark.parametrize("irregular", [False, True])
 def test_early_stop_stops_only_on_codewords(torch, irregular):
     """Syndrome early stop: a frame that stops before max_iters must carry a valid
     codeword (for the regular distinct-column code the all-zero one; the irregular
