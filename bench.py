@@ -569,6 +569,22 @@ def main():
             "trials_per_s": Be / (a.elapsed_time(b) * 1e-3), "batch": Be, "mean_iterations": float(cnt[3] / cnt[0]),
             "frame_errors": int(cnt[1]), "trials": int(cnt[0])}
         del mc
+        # the same at the FER campaigns' batch (scripts/fer_campaign.sh: 65,536 graphs per launch,
+        # ~100 GB of edge lists): the sampler's tail (the last graphs' helpers) amortised 4x
+        Bc = 65536
+        mc = MonteCarlo.ensemble(64800, DV, DC, "bec", 0.42, 200, seed=7, batch=Bc, expurgation=3)
+        mc.run_batch(0, 256)
+        torch.cuda.synchronize()
+        a.record(stream)
+        mc.run_batch(256, Bc)
+        b.record(stream)
+        torch.cuda.synchronize()
+        cnt = mc.counters.cpu().numpy()
+        extras["ensemble_mc_cfg5_n64800_eps0.42_200it_X3_campaign_batch"] = {
+            "trials_per_s": Bc / (a.elapsed_time(b) * 1e-3), "batch": Bc, "mean_iterations": float(cnt[3] / cnt[0]),
+            "frame_errors": int(cnt[1]), "trials": int(cnt[0])}
+        del mc
+        torch.cuda.empty_cache()
         # "optimal" modes: ML erasure decoding (parallel_simulator.py:60-129), n = 1000, eps = 0.45
         gm = TannerGraph.random_regular(1000, DV, DC, seed=1)
         wm = decoder.channel_dev("bec", 0.45, 5, 0, gm.n, 32768)
