@@ -153,8 +153,7 @@ constexpr int kSeqRing = 512;                  // ring: a round + the longest ch
 static_assert(kSeqSlots + kSeqMaxCdeg <= kSeqRing, "the ring must hold a round and the check it completes");
 static_assert(kSeqNW == 2, "the cut words hold two waves");
 static_assert(kSeqMaxE <= (1 << 19), "first-pass keys: an entry in 19 bits, the word index above bit 20");
-// LDS sync words of an attempt: reject flags by round parity, cut[parity][wave], claim broadcast
-// LDS sync words: reject flags by round parity [0, 2), per parity and wave the two lowest
+// LDS sync words of an attempt: reject flags by round parity [0, 2), per parity and wave the two lowest
 // colliding slots and the lowest one's pick [2, 14), the pick's owner per wave [14, 16), the
 // claim broadcast [16, 19)
 enum { kSyFlag = 0, kSyCut = 2, kSyOwn = 14, kSyClaim = 16, kSeqSync = 24 };
